@@ -1,0 +1,358 @@
+// api.hip -- extern "C" entry points of libgslm.so (declared in include/gslm.h).
+#include <cstring>
+#include <string>
+#include "gslm_kernels.hpp"
+
+namespace gslm {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t count) {
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off = align_up(off + count * sizeof(T));
+    return p;
+  }
+};
+
+__global__ void k_iota(uint32_t* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)i;
+}
+
+}  // namespace
+
+size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
+  Carver c{(char*)base};
+  GeomBufs g;
+  g.rec = c.take<float4>((size_t)P * REC_F4);
+  g.depth_key = c.take<uint32_t>(P);
+  g.tiles = c.take<uint32_t>(P);
+  g.rect = c.take<uint2>(P);
+  g.vals_init = c.take<uint32_t>(P);
+  g.sorted_idx = g.vals_init;
+  g.keys_alt = c.take<uint32_t>(P);
+  g.vals_alt = c.take<uint32_t>(P);
+  g.offsets = c.take<uint32_t>(P);
+  g.offset_by_g = c.take<uint32_t>(P);
+  g.hist = c.take<uint32_t>(sort_hist_bytes(P) / 4);
+  g.scan_tmp = c.take<uint32_t>(scan_tmp_bytes(P) / 4);
+  g.counters = c.take<uint32_t>(16);
+  if (o) *o = g;
+  return c.off;
+}
+
+size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
+  Carver c{(char*)base};
+  BinBufs b;
+  b.keys0 = c.take<uint32_t>(N);
+  b.keys1 = c.take<uint32_t>(N);
+  b.vals0 = c.take<uint32_t>(N);
+  b.vals1 = c.take<uint32_t>(N);
+  b.gid = c.take<uint32_t>(N);
+  b.point_list = c.take<uint32_t>(N);
+  b.inv = c.take<uint32_t>(N);
+  b.hist = c.take<uint32_t>(sort_hist_bytes(N) / 4);
+  b.ranges = c.take<uint2>(ntiles);
+  if (o) *o = b;
+  return c.off;
+}
+
+size_t img_layout(int H, int W, void* base, ImgBufs* o) {
+  Carver c{(char*)base};
+  ImgBufs b;
+  b.final_T = c.take<float>((size_t)H * W);
+  b.n_contrib = c.take<uint32_t>((size_t)H * W);
+  if (o) *o = b;
+  return c.off;
+}
+
+size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* o) {
+  Carver c{(char*)base};
+  ScratchBufs b;
+  b.trec = c.take<float4>((size_t)P * REC_F4);
+  b.contrib = c.take<float4>((size_t)N * REC_F4);
+  if (o) *o = b;
+  return c.off;
+}
+
+static int make_view(const gslm_view* in, int M, ViewK* v) {
+  if (!in) { set_error("view is NULL"); return GSLM_ERR_INVALID; }
+  if (in->image_height <= 0 || in->image_width <= 0) { set_error("image size must be positive"); return GSLM_ERR_INVALID; }
+  if (in->image_height > 65535 * 16 || in->image_width > 65535 * 16) { set_error("image too large"); return GSLM_ERR_INVALID; }
+  if (in->sh_degree < 0 || in->sh_degree > 3) { set_error("sh_degree must be in [0,3]"); return GSLM_ERR_INVALID; }
+  if (!(in->tanfovx > 0.0) || !(in->tanfovy > 0.0)) { set_error("tanfov must be positive"); return GSLM_ERR_INVALID; }
+  v->H = in->image_height;
+  v->W = in->image_width;
+  v->gx = (v->W + TILE_X - 1) / TILE_X;
+  v->gy = (v->H + TILE_Y - 1) / TILE_Y;
+  v->focal_x = (float)((double)v->W / (2.0 * in->tanfovx));
+  v->focal_y = (float)((double)v->H / (2.0 * in->tanfovy));
+  v->limx = (float)(1.3 * in->tanfovx);
+  v->limy = (float)(1.3 * in->tanfovy);
+  std::memcpy(v->view, in->viewmatrix, sizeof(v->view));
+  std::memcpy(v->proj, in->projmatrix, sizeof(v->proj));
+  for (int k = 0; k < 3; ++k) { v->campos[k] = in->campos[k]; v->bg[k] = in->bg[k]; }
+  v->scale_mod = (float)in->scale_modifier;
+  v->D = in->sh_degree;
+  v->M = M;
+  v->antialiasing = in->antialiasing ? 1 : 0;
+  return GSLM_OK;
+}
+
+static int make_gauss(const gslm_gaussians* in, const ViewK* v, GaussK* g, bool tangent) {
+  if (!in) { set_error("gaussians is NULL"); return GSLM_ERR_INVALID; }
+  if (in->P < 0 || in->P > 0x7FFFFFFFll) { set_error("P out of range"); return GSLM_ERR_INVALID; }
+  g->P = in->P;
+  g->raw = in->raw ? 1 : 0;
+  g->M = in->max_coeffs;
+  g->means3D = in->means3D;
+  g->opac = in->opacities;
+  g->scales = in->scales;
+  g->rot = in->rotations;
+  g->cov3D = in->cov3D_precomp;
+  g->dc = in->sh_dc;
+  g->dc_stride = in->sh_dc_stride;
+  g->rest = in->sh_rest;
+  g->rest_stride = in->sh_rest_stride;
+  g->colors = in->colors_precomp;
+  if (tangent || in->P == 0) return GSLM_OK;
+  if (!g->means3D || !g->opac) { set_error("means3D and opacities are required"); return GSLM_ERR_INVALID; }
+  if (!g->cov3D && !(g->scales && g->rot)) { set_error("need scales+rotations or cov3D_precomp"); return GSLM_ERR_INVALID; }
+  if (!g->colors) {
+    if (!g->dc) { set_error("need shs or colors_precomp"); return GSLM_ERR_INVALID; }
+    if ((v->D + 1) * (v->D + 1) > g->M) { set_error("sh_degree exceeds stored coefficients"); return GSLM_ERR_INVALID; }
+    if (g->M > 1 && !g->rest) { set_error("sh_rest is NULL"); return GSLM_ERR_INVALID; }
+  }
+  return GSLM_OK;
+}
+
+int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* radii, hipStream_t s) {
+  int st = launch_preprocess(v, g, gb, radii, s);
+  if (st) return st;
+  const int64_t P = g.P;
+  if (P == 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(gb.counters, 0, 4, s));
+    return GSLM_OK;
+  }
+  hipLaunchKernelGGL(k_iota, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, gb.vals_init, P);
+  GSLM_LAUNCH_CHECK();
+  bool alt = false;
+  st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s);
+  if (st) return st;
+  if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  return exclusive_scan_u32(gb.tiles, gb.sorted_idx, gb.offsets, P, gb.scan_tmp, gb.counters, s);
+}
+
+}  // namespace gslm
+
+using namespace gslm;
+
+extern "C" {
+
+const char* gslm_last_error(void) { return g_last_error.c_str(); }
+int gslm_abi_version(void) { return GSLM_ABI_VERSION; }
+
+size_t gslm_geom_bytes(int64_t P) { return geom_layout(P, nullptr, nullptr); }
+size_t gslm_image_bytes(int32_t H, int32_t W) { return img_layout(H, W, nullptr, nullptr); }
+size_t gslm_binning_bytes(int64_t N, int32_t H, int32_t W) {
+  const int ntiles = ((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y);
+  return bin_layout(N, ntiles, nullptr, nullptr);
+}
+size_t gslm_scratch_bytes(int64_t P, int64_t N) { return scratch_layout(P, N, nullptr, nullptr); }
+
+int gslm_preprocess(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, int32_t* out_radii,
+                    void* stream) {
+  ViewK v;
+  GaussK g;
+  int st = make_view(view, gi ? gi->max_coeffs : 0, &v);
+  if (st) return st;
+  if ((st = make_gauss(gi, &v, &g, false))) return st;
+  if (geom_bytes < gslm_geom_bytes(g.P) || (!geom && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
+  GeomBufs gb;
+  geom_layout(g.P, geom, &gb);
+  return do_preprocess(v, g, gb, out_radii, (hipStream_t)stream);
+}
+
+int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
+  GeomBufs gb;
+  geom_layout(P, const_cast<void*>(geom), &gb);
+  uint32_t h = 0;
+  GSLM_HIP_CHECK(hipMemcpyAsync(&h, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  GSLM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  *out = (int64_t)h;
+  return GSLM_OK;
+}
+
+int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                   int64_t N, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
+                   void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (binning_bytes < gslm_binning_bytes(N, v.H, v.W)) { set_error("binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (image_bytes < gslm_image_bytes(v.H, v.W)) { set_error("image workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (!out_color) { set_error("out_color is NULL"); return GSLM_ERR_INVALID; }
+  GeomBufs gb;
+  BinBufs bb;
+  ImgBufs ib;
+  geom_layout(P, geom, &gb);
+  bin_layout(N, v.gx * v.gy, binning, &bb);
+  img_layout(v.H, v.W, image, &ib);
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = launch_binning(v, P, gb, bb, N, s))) return st;
+  return launch_render_fwd(v, gb, bb, ib, out_color, out_invdepth, s);
+}
+
+int gslm_forward(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, void* binning,
+                 size_t binning_bytes, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
+                 int32_t* out_radii, int64_t* out_num_rendered, void* stream) {
+  int st = gslm_preprocess(view, gi, geom, geom_bytes, out_radii, stream);
+  if (st) return st;
+  int64_t N = 0;
+  if ((st = gslm_num_rendered(geom, gi->P, &N, stream))) return st;
+  if (out_num_rendered) *out_num_rendered = N;
+  if (binning_bytes < gslm_binning_bytes(N, view->image_height, view->image_width)) {
+    set_error("binning workspace too small for num_rendered");
+    return GSLM_ERR_CAPACITY;
+  }
+  return gslm_rasterize(view, gi->P, geom, binning, binning_bytes, N, image, image_bytes, out_color, out_invdepth,
+                        stream);
+}
+
+
+static GradK make_gradk(const gslm_grads* o) {
+  GradK k;
+  k.means2D = o->means2D;
+  k.means3D = o->means3D;
+  k.opac = o->opacities;
+  k.scales = o->scales;
+  k.rot = o->rotations;
+  k.cov3D = o->cov3D;
+  k.dc = o->sh_dc;
+  k.dc_stride = o->sh_dc_stride;
+  k.rest = o->sh_rest;
+  k.rest_stride = o->sh_rest_stride;
+  k.colors = o->colors;
+  k.accumulate = o->accumulate;
+  return k;
+}
+
+static GaussK tangent_from_grads(const gslm_grads* t, const GaussK& g, bool mask_xyz) {
+  GaussK k;
+  k.P = g.P;
+  k.raw = g.raw;
+  k.M = g.M;
+  k.means3D = mask_xyz ? nullptr : t->means3D;
+  k.opac = t->opacities;
+  k.scales = t->scales;
+  k.rot = t->rotations;
+  k.cov3D = t->cov3D;
+  k.dc = t->sh_dc;
+  k.dc_stride = t->sh_dc_stride;
+  k.rest = t->sh_rest;
+  k.rest_stride = t->sh_rest_stride;
+  k.colors = t->colors;
+  return k;
+}
+
+struct Bound {
+  ViewK v;
+  GaussK g;
+  GeomBufs gb;
+  BinBufs bb;
+  ImgBufs ib;
+  ScratchBufs sb;
+};
+
+static int bind_all(const gslm_view* view, const gslm_gaussians* gi, const void* geom, const void* binning,
+                    int64_t N, const void* image, void* scratch, size_t scratch_bytes, Bound* b) {
+  int st = make_view(view, gi ? gi->max_coeffs : 0, &b->v);
+  if (st) return st;
+  if ((st = make_gauss(gi, &b->v, &b->g, false))) return st;
+  if (scratch_bytes < gslm_scratch_bytes(b->g.P, N)) {
+    set_error("scratch workspace too small");
+    return GSLM_ERR_CAPACITY;
+  }
+  geom_layout(b->g.P, const_cast<void*>(geom), &b->gb);
+  bin_layout(N, b->v.gx * b->v.gy, const_cast<void*>(binning), &b->bb);
+  img_layout(b->v.H, b->v.W, const_cast<void*>(image), &b->ib);
+  scratch_layout(b->g.P, N, scratch, &b->sb);
+  return GSLM_OK;
+}
+
+int gslm_backward(const gslm_view* view, const gslm_gaussians* gi, const void* geom, const void* binning, int64_t N,
+                  const void* image, const float* dL_dcolor, const float* dL_dinvdepth, void* scratch,
+                  size_t scratch_bytes, const gslm_grads* out, void* stream) {
+  Bound b;
+  int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
+  if (st) return st;
+  if (!out || !dL_dcolor) { set_error("backward: NULL dL_dcolor or outputs"); return GSLM_ERR_INVALID; }
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = launch_render_bwd(b.v, b.gb, b.bb, b.ib, N, dL_dcolor, dL_dinvdepth, b.sb, s))) return st;
+  return launch_preprocess_bwd(b.v, b.g, b.gb, b.bb, b.sb, make_gradk(out), true, s);
+}
+
+int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussians* tangent,
+             const float* means2D_tangent, const void* geom, const void* binning, int64_t N, const void* image,
+             void* scratch, size_t scratch_bytes, float* out_color_t, float* out_invdepth_t, void* stream) {
+  Bound b;
+  int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
+  if (st) return st;
+  if (!out_color_t) { set_error("jvp: NULL out_color_t"); return GSLM_ERR_INVALID; }
+  GaussK t;
+  if ((st = make_gauss(tangent, &b.v, &t, true))) return st;
+  t.P = b.g.P;
+  t.raw = b.g.raw;
+  t.M = b.g.M;
+  return launch_jvp(b.v, b.g, t, means2D_tangent, b.gb, b.bb, b.ib, b.sb, out_color_t, out_invdepth_t,
+                    (hipStream_t)stream);
+}
+
+int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
+                     const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning, int64_t N,
+                     const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y, void* stream) {
+  Bound b;
+  int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
+  if (st) return st;
+  if (!vin || !y || !pixel_weight) { set_error("matvec: NULL argument"); return GSLM_ERR_INVALID; }
+  hipStream_t s = (hipStream_t)stream;
+  const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
+  if ((st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, s))) return st;
+  if (N > 0 && (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s))) return st;
+  GradK yk = make_gradk(y);
+  yk.accumulate = 1;
+  yk.means2D = nullptr;
+  if (mask_xyz) yk.means3D = nullptr;
+  if (N == 0) return GSLM_OK;
+  return launch_preprocess_bwd(b.v, b.g, b.gb, b.bb, b.sb, yk, mask_xyz == 0, s);
+}
+
+int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, int32_t H, int32_t W,
+                 const void* image, uint32_t* point_list, uint32_t* ranges, uint32_t* tiles_touched, float* final_T,
+                 uint32_t* n_contrib, float* records, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  GeomBufs gb;
+  BinBufs bb;
+  ImgBufs ib;
+  const int ntiles = ((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y);
+  geom_layout(P, const_cast<void*>(geom), &gb);
+  bin_layout(N, ntiles, const_cast<void*>(binning), &bb);
+  img_layout(H, W, const_cast<void*>(image), &ib);
+  const auto D2D = hipMemcpyDeviceToDevice;
+  if (point_list && N) GSLM_HIP_CHECK(hipMemcpyAsync(point_list, bb.point_list, (size_t)N * 4, D2D, s));
+  if (ranges && binning) GSLM_HIP_CHECK(hipMemcpyAsync(ranges, bb.ranges, (size_t)ntiles * 8, D2D, s));
+  if (tiles_touched && P) GSLM_HIP_CHECK(hipMemcpyAsync(tiles_touched, gb.tiles, (size_t)P * 4, D2D, s));
+  if (final_T && image) GSLM_HIP_CHECK(hipMemcpyAsync(final_T, ib.final_T, (size_t)H * W * 4, D2D, s));
+  if (n_contrib && image) GSLM_HIP_CHECK(hipMemcpyAsync(n_contrib, ib.n_contrib, (size_t)H * W * 4, D2D, s));
+  if (records && P) GSLM_HIP_CHECK(hipMemcpyAsync(records, gb.rec, (size_t)P * 48, D2D, s));
+  return GSLM_OK;
+}
+
+}  // extern "C"

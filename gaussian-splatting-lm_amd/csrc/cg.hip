@@ -1,0 +1,166 @@
+// cg.hip -- device-resident vector algebra for the CG / CGLS drivers on flat param-space vectors.
+//
+// Replaces GaussianModelState.dot / __add__ / __mul__ (solver/gaussian_model_state.py:197-273),
+// whose every dot ends in `.item()` (a host sync per dot).  Here scalars stay in device memory
+// (double) and the step sizes alpha = gamma / delta, beta = gamma' / gamma are read by the update
+// kernels directly, so a CG iteration issues no host synchronisation.  Reductions are two-pass
+// with a fixed block/thread assignment: deterministic.
+#include "gslm_internal.hpp"
+
+namespace gslm {
+
+constexpr int MAXG = 8;
+struct Groups {
+  int64_t bound[MAXG + 1];
+  double damp[MAXG];
+  int n;
+};
+
+constexpr int DOT_THREADS = 256;
+constexpr int DOT_BLOCKS = 1024;
+
+__device__ __forceinline__ double group_w(const Groups& g, int64_t i) {
+  double w = 1.0;
+  if (g.n > 0) {
+    w = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAXG; ++k)
+      if (k < g.n && i >= g.bound[k] && i < g.bound[k + 1]) w = g.damp[k];
+  }
+  return w;
+}
+
+__device__ __forceinline__ double block_sum_d(double x, double* s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+  if (lane == 0) s[w] = x;
+  __syncthreads();
+  double t = 0.0;
+  if (tid == 0)
+    for (int k = 0; k < DOT_THREADS / 64; ++k) t += s[k];
+  return t;
+}
+
+__global__ __launch_bounds__(DOT_THREADS) void k_dot_partial(const float* __restrict__ a, const float* __restrict__ b,
+                                                             Groups g, int64_t n, double* __restrict__ part) {
+  __shared__ double s[DOT_THREADS / 64];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * DOT_THREADS;
+  if (g.n == 0) {
+    for (int64_t i = (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n; i += stride)
+      acc += (double)a[i] * (double)b[i];
+  } else {
+    for (int k = 0; k < g.n; ++k) {
+      double gacc = 0.0;
+      const int64_t lo = g.bound[k], hi = min(g.bound[k + 1], n);
+      // align the group start to the grid so each element is visited by exactly one thread
+      for (int64_t i = lo + (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < hi; i += stride)
+        gacc += (double)a[i] * (double)b[i];
+      acc += g.damp[k] * gacc;
+    }
+  }
+  const double t = block_sum_d(acc, s);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(DOT_THREADS) void k_dot_final(const double* __restrict__ part, int np,
+                                                           double* __restrict__ out) {
+  __shared__ double s[DOT_THREADS / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += DOT_THREADS) acc += part[i];
+  const double t = block_sum_d(acc, s);
+  if (threadIdx.x == 0) *out = t;
+}
+
+__global__ __launch_bounds__(256) void k_axpy_dev(int64_t n, const double* __restrict__ num,
+                                                  const double* __restrict__ den, float sign,
+                                                  const float* __restrict__ x, float* __restrict__ y) {
+  const double a = den ? (*num) / (*den) : (*num);
+  const float af = (float)(a * (double)sign);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = y[i] + af * x[i];
+}
+
+__global__ __launch_bounds__(256) void k_xpby_dev(int64_t n, const float* __restrict__ s, const double* __restrict__ num,
+                                                  const double* __restrict__ den, float* __restrict__ p) {
+  const float b = (float)((*num) / (*den));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = s[i] + b * p[i];
+}
+
+__global__ __launch_bounds__(256) void k_damp_add(int64_t n, const float* __restrict__ x, Groups g,
+                                                  float* __restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = y[i] + (float)group_w(g, i) * x[i];
+}
+
+static int make_groups(const int64_t* bounds, const double* damp, int ng, Groups* g) {
+  if (ng < 0 || ng > MAXG) {
+    set_error("at most 8 damping groups");
+    return GSLM_ERR_INVALID;
+  }
+  g->n = ng;
+  for (int k = 0; k <= MAXG; ++k) g->bound[k] = (k <= ng && bounds) ? bounds[k] : 0;
+  for (int k = 0; k < MAXG; ++k) g->damp[k] = (k < ng && damp) ? damp[k] : 0.0;
+  return GSLM_OK;
+}
+
+static unsigned grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace gslm
+
+using namespace gslm;
+
+extern "C" {
+
+size_t gslm_dot_scratch_bytes(int64_t n) {
+  (void)n;
+  return DOT_BLOCKS * sizeof(double);
+}
+
+int gslm_dot(const float* a, const float* b, const int64_t* group_bounds, const double* group_damp, int32_t ngroups,
+             int64_t n, void* scratch, double* out_dev, void* stream) {
+  Groups g;
+  int st = make_groups(group_bounds, group_damp, ngroups, &g);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_dot_partial, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, s, a, b, g, n, (double*)scratch);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, s, (const double*)scratch, DOT_BLOCKS, out_dev);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_axpy_dev(int64_t n, const double* num_dev, const double* den_dev, float sign, const float* x, float* y,
+                  void* stream) {
+  if (n <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_axpy_dev, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, num_dev, den_dev, sign, x, y);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_xpby_dev(int64_t n, const float* s_, const double* num_dev, const double* den_dev, float* p, void* stream) {
+  if (n <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_xpby_dev, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, s_, num_dev, den_dev, p);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const double* group_damp, int32_t ngroups,
+                  float* y, void* stream) {
+  Groups g;
+  int st = make_groups(group_bounds, group_damp, ngroups, &g);
+  if (st) return st;
+  if (n <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_damp_add, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, g, y);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+// forward.hip -- rasterizer forward for gfx950.
+//
+//   k_preprocess   one thread per Gaussian: cull, project, cov3D, EWA cov2D, conic, radius,
+//                  rect, SH->RGB; writes a 48-B render record + depth key + tile count.
+//   (depth sort of P keys + scan of tile counts in depth order: sort.hip)
+//   k_duplicate    emits (tile id, dup index) pairs in depth order: the later *stable* sort on
+//                  the tile id alone then yields upstream's (tile, depth, index) order with
+//                  2 radix passes over N_dup instead of 6 (SURVEY §7 "Sort").
+//   k_finalize     point_list[k] = gid(dup[k]), inv[dup[k]] = k (slot of each dup entry).
+//   k_ranges       per-tile [start, end) from key changes (identifyTileRanges).
+//   k_render_fwd   one 16x16 tile per 256-thread block (4 wave64), Gaussian records staged
+//                  through LDS 256 at a time, __syncthreads_count early exit (renderCUDA).
+#include "gslm_internal.hpp"
+#include "gslm_kernels.hpp"
+
+namespace gslm {
+
+template <bool RAW>
+__global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* __restrict__ rec,
+                                                     uint32_t* __restrict__ depth_key,
+                                                     uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
+                                                     int* __restrict__ radii_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.P) return;
+  tiles[i] = 0u;
+  depth_key[i] = 0xFFFFFFFFu;
+  if (radii_out) radii_out[i] = 0;
+  PreOut o;
+  if (!preprocess_one<RAW>(v, g, i, o)) return;
+
+  const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
+  const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
+  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.depth);
+  rec[3 * i + 0] = r0;
+  rec[3 * i + 1] = r1;
+  rec[3 * i + 2] = r2;
+  depth_key[i] = __float_as_uint(o.depth);
+  tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
+  rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  if (radii_out) radii_out[i] = o.radius;
+}
+
+__global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
+                                                    const uint32_t* __restrict__ offsets,
+                                                    const uint32_t* __restrict__ tiles,
+                                                    const uint2* __restrict__ rect, uint32_t* __restrict__ offset_by_g,
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    uint32_t* __restrict__ gid) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P) return;
+  const uint32_t g = sorted_idx[s];
+  const uint32_t n = tiles[g];
+  uint32_t off = offsets[s];
+  offset_by_g[g] = off;
+  if (n == 0) return;
+  const uint2 rc = rect[g];
+  const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
+  for (int ty = y0; ty < y1; ++ty)
+    for (int tx = x0; tx < x1; ++tx) {
+      keys[off] = (uint32_t)(ty * gx + tx);
+      vals[off] = off;
+      gid[off] = g;
+      ++off;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(int64_t N, const uint32_t* __restrict__ sorted_dup,
+                                                   const uint32_t* __restrict__ gid,
+                                                   uint32_t* __restrict__ point_list, uint32_t* __restrict__ inv) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const uint32_t d = sorted_dup[k];
+  point_list[k] = gid[d];
+  inv[d] = (uint32_t)k;
+}
+
+__global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __restrict__ keys,
+                                                 uint2* __restrict__ ranges) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const uint32_t t = keys[k];
+  if (k == 0 || keys[k - 1] != t) ranges[t].x = (uint32_t)k;
+  if (k == N - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
+}
+
+// renderCUDA forward.  Pixel (px,py) of the tile is thread ty*16+tx: wave w holds rows 4w..4w+3.
+__global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
+                                                     const uint32_t* __restrict__ point_list,
+                                                     const float4* __restrict__ rec, float* __restrict__ out_color,
+                                                     float* __restrict__ out_invdepth, float* __restrict__ final_T,
+                                                     uint32_t* __restrict__ n_contrib) {
+  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_r2[TILE_PIX];
+  const int tile = blockIdx.x;
+  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
+  const int tid = threadIdx.x;
+  const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
+  const bool inside = px < v.W && py < v.H;
+  const float pxf = (float)px, pyf = (float)py;
+  bool done = !inside;
+  const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
+  const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
+
+  float T = 1.0f;
+  uint32_t contributor = 0, last = 0;
+  float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+  int todo = n;
+  for (int r = 0; r < rounds; ++r, todo -= TILE_PIX) {
+    const int num_done = __syncthreads_count(done);
+    if (num_done == TILE_PIX) break;
+    const int k = r * TILE_PIX + tid;
+    if (k < n) {
+      const uint32_t gidx = point_list[range.x + k];
+      s_r0[tid] = rec[3 * (int64_t)gidx + 0];
+      s_r1[tid] = rec[3 * (int64_t)gidx + 1];
+      s_r2[tid] = rec[3 * (int64_t)gidx + 2];
+    }
+    __syncthreads();
+    const int cnt = min(TILE_PIX, todo);
+    for (int j = 0; !done && j < cnt; ++j) {
+      ++contributor;
+      const float4 a = s_r0[j];
+      const float4 b = s_r1[j];
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      if (power > 0.0f) continue;
+      const float alpha = fminf(0.99f, b.y * expf(power));
+      if (alpha < 1.0f / 255.0f) continue;
+      const float test_T = T * (1.0f - alpha);
+      if (test_T < 0.0001f) {
+        done = true;
+        continue;
+      }
+      const float4 c = s_r2[j];
+      const float w = alpha * T;
+      C0 += b.z * w;
+      C1 += b.w * w;
+      C2 += c.x * w;
+      Dp += c.y * w;
+      T = test_T;
+      last = contributor;
+    }
+  }
+  if (inside) {
+    const int64_t pid = (int64_t)py * v.W + px;
+    const int64_t HW = (int64_t)v.H * v.W;
+    final_T[pid] = T;
+    n_contrib[pid] = last;
+    out_color[pid] = C0 + T * v.bg[0];
+    out_color[HW + pid] = C1 + T * v.bg[1];
+    out_color[2 * HW + pid] = C2 + T * v.bg[2];
+    if (out_invdepth) out_invdepth[pid] = Dp;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s) {
+  if (g.P == 0) return GSLM_OK;
+  const int nb = (int)((g.P + 255) / 256);
+  if (g.raw)
+    hipLaunchKernelGGL(k_preprocess<true>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles, gb.rect,
+                       radii_out);
+  else
+    hipLaunchKernelGGL(k_preprocess<false>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles, gb.rect,
+                       radii_out);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
+  if (P > 0)
+    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
+                       gb.offsets, gb.tiles, gb.rect, gb.offset_by_g, bb.keys0, bb.vals0, bb.gid);
+  GSLM_LAUNCH_CHECK();
+  if (N == 0) return GSLM_OK;
+  int end_bit = 0;
+  while ((1ll << end_bit) < (long long)ntiles) ++end_bit;
+  if (end_bit == 0) end_bit = 1;
+  bool alt = false;
+  int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, end_bit, bb.hist, &alt, s);
+  if (st != GSLM_OK) return st;
+  const uint32_t* skeys = alt ? bb.keys1 : bb.keys0;
+  const uint32_t* svals = alt ? bb.vals1 : bb.vals0;
+  const unsigned nbN = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_finalize, dim3(nbN), dim3(256), 0, s, N, svals, bb.gid, bb.point_list, bb.inv);
+  hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, skeys, bb.ranges);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
+                      float* out_invdepth, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (ntiles == 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_render_fwd, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list, gb.rec,
+                     out_color, out_invdepth, ib.final_T, ib.n_contrib);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+}  // namespace gslm

@@ -1,0 +1,58 @@
+// gslm_internal.hpp -- host-side internal interfaces between the .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include "gslm.h"
+#include "gslm_device.hpp"
+
+namespace gslm {
+
+void set_error(const std::string& msg);
+
+#define GSLM_HIP_CHECK(expr)                                                                  \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) {                                                                   \
+      ::gslm::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+      return GSLM_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
+#define GSLM_LAUNCH_CHECK()                                                                   \
+  do {                                                                                        \
+    hipError_t _e = hipGetLastError();                                                        \
+    if (_e != hipSuccess) {                                                                   \
+      ::gslm::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));              \
+      return GSLM_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// ---------------- radix sort (LSD, 8-bit digits, stable) ----------------
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 16;                       // items per thread per block
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS; // 4096 keys per block
+constexpr int RADIX = 256;
+
+inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_blocks(n) * 4 + 4 * RADIX; }
+
+// Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
+// ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
+int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s);
+
+// ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+inline int64_t scan_blocks(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n) * 4 + 64); }
+// out[i] = sum_{j<i} in[idx ? idx[j] : j];  *total (device) = full sum.
+int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
+                       uint32_t* total, hipStream_t s);
+
+}  // namespace gslm

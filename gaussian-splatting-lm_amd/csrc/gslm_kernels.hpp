@@ -1,0 +1,201 @@
+// gslm_kernels.hpp -- device structs, per-Gaussian preprocess routine, workspace views, launchers.
+#pragma once
+#include "gslm_internal.hpp"
+
+namespace gslm {
+
+// Device view of gslm_gaussians (also used for tangents: NULL pointer = zero tangent).
+struct GaussK {
+  int64_t P;
+  int raw;
+  int M;
+  const float* means3D;
+  const float* opac;
+  const float* scales;
+  const float* rot;
+  const float* cov3D;
+  const float* dc;
+  int64_t dc_stride;
+  const float* rest;
+  int64_t rest_stride;
+  const float* colors;
+  __device__ __forceinline__ float sh(int64_t i, int k, int c) const {
+    return k == 0 ? dc[i * dc_stride + c] : rest[i * rest_stride + 3 * (k - 1) + c];
+  }
+};
+
+// Device view of gslm_grads.
+struct GradK {
+  float* means2D;
+  float* means3D;
+  float* opac;
+  float* scales;
+  float* rot;
+  float* cov3D;
+  float* dc;
+  int64_t dc_stride;
+  float* rest;
+  int64_t rest_stride;
+  float* colors;
+  int accumulate;
+};
+
+struct PreOut {
+  float x, y;
+  float conic[3];
+  float opac;
+  float rgb[3];
+  float depth;
+  uint32_t clamped;
+  int radius;
+  int rmin_x, rmin_y, rmax_x, rmax_y;
+};
+
+// Activated scale / rotation of Gaussian i (fusing exp / normalize when RAW).
+template <bool RAW>
+__device__ __forceinline__ void load_scale_rot(const GaussK& g, int64_t i, float s[3], float q[4]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = RAW ? expf(g.scales[3 * i + k]) : g.scales[3 * i + k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = g.rot[4 * i + k];
+  if (RAW) {
+    const float nrm = fmaxf(sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]), 1e-12f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = q[k] / nrm;
+  }
+}
+
+// SURVEY Appendix A steps 1-9 for one Gaussian; returns false when culled.
+template <bool RAW>
+__device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, int64_t i, PreOut& o) {
+  const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
+  const float tz = tp_row(v.view, x, y, z, 2);
+  if (!(tz > 0.2f)) return false;
+  const float tx = tp_row(v.view, x, y, z, 0), ty = tp_row(v.view, x, y, z, 1);
+  const float hx = tp_row(v.proj, x, y, z, 0), hy = tp_row(v.proj, x, y, z, 1), hw = tp_row(v.proj, x, y, z, 3);
+  const float p_w = 1.0f / (hw + 0.0000001f);
+  const float pxn = hx * p_w, pyn = hy * p_w;
+
+  float c[6];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c[k] = g.cov3D[6 * i + k];
+  } else {
+    float s[3], q[4], R[9];
+    load_scale_rot<RAW>(g, i, s, q);
+    quat_rot(q[0], q[1], q[2], q[3], R);
+    cov3d_from(v.scale_mod * s[0], v.scale_mod * s[1], v.scale_mod * s[2], R, c);
+  }
+  Proj2 pj;
+  ewa_jacobian(v, tx, ty, tz, pj);
+  float c00 = quad_form(pj.A0, c, pj.A0);
+  const float c01 = quad_form(pj.A0, c, pj.A1);
+  float c11 = quad_form(pj.A1, c, pj.A1);
+  const float det0 = c00 * c11 - c01 * c01;
+  c00 = c00 + 0.3f;
+  c11 = c11 + 0.3f;
+  const float det = c00 * c11 - c01 * c01;
+  float h = 1.0f;
+  if (v.antialiasing) h = sqrtf(fmaxf(0.000025f, det0 / det));
+  if (det == 0.0f) return false;
+  const float det_inv = 1.0f / det;
+  o.conic[0] = c11 * det_inv;
+  o.conic[1] = -c01 * det_inv;
+  o.conic[2] = c00 * det_inv;
+  const float mid = 0.5f * (c00 + c11);
+  const float lam1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float radius = ceilf(3.0f * sqrtf(lam1));
+  o.x = ndc2pix(pxn, v.W);
+  o.y = ndc2pix(pyn, v.H);
+  o.rmin_x = min(v.gx, max(0, trunc_i((o.x - radius) / 16.0f)));
+  o.rmin_y = min(v.gy, max(0, trunc_i((o.y - radius) / 16.0f)));
+  o.rmax_x = min(v.gx, max(0, trunc_i((((o.x + radius) + 16.0f) - 1.0f) / 16.0f)));
+  o.rmax_y = min(v.gy, max(0, trunc_i((((o.y + radius) + 16.0f) - 1.0f) / 16.0f)));
+  if ((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y) == 0) return false;
+
+  o.clamped = 0u;
+  if (g.colors) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.rgb[k] = g.colors[3 * i + k];
+  } else {
+    float dx = x - v.campos[0], dy = y - v.campos[1], dz = z - v.campos[2];
+    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    auto shf = [&](int k, int ch) { return g.sh(i, k, ch); };
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float r = sh_color(v.D, dx, dy, dz, shf, ch);
+      if (r < 0.0f) o.clamped |= (1u << ch);
+      o.rgb[ch] = fmaxf(r, 0.0f);
+    }
+  }
+  const float op = RAW ? sigmoidf_(g.opac[i]) : g.opac[i];
+  o.opac = op * h;
+  o.depth = tz;
+  o.radius = (int)radius;
+  return true;
+}
+
+// ---------------- workspace views ----------------
+struct GeomBufs {
+  float4* rec;            // [P*3]
+  uint32_t* depth_key;    // [P]
+  uint32_t* tiles;        // [P]
+  uint2* rect;            // [P]
+  uint32_t* sorted_idx;   // [P] Gaussian ids in depth order (after sort)
+  uint32_t* keys_alt;     // [P]
+  uint32_t* vals_alt;     // [P]
+  uint32_t* vals_init;    // [P] identity
+  uint32_t* offsets;      // [P] exclusive scan of tiles in depth order
+  uint32_t* offset_by_g;  // [P] dup start of Gaussian g
+  uint32_t* hist;         // radix histogram
+  uint32_t* scan_tmp;     // scan block sums
+  uint32_t* counters;     // [0] = num_rendered
+};
+struct BinBufs {
+  uint32_t* keys0;
+  uint32_t* keys1;
+  uint32_t* vals0;
+  uint32_t* vals1;
+  uint32_t* gid;
+  uint32_t* point_list;
+  uint32_t* inv;
+  uint32_t* hist;
+  uint2* ranges;
+};
+struct ImgBufs {
+  float* final_T;
+  uint32_t* n_contrib;
+};
+struct ScratchBufs {
+  float4* trec;   // [P*3] tangent render records
+  float4* contrib; // [N*3] per (tile, Gaussian) reduced gradient rows
+};
+
+size_t geom_layout(int64_t P, void* base, GeomBufs* out);
+size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* out);
+size_t img_layout(int H, int W, void* base, ImgBufs* out);
+size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
+
+int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
+int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
+int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
+                      float* out_invdepth, hipStream_t s);
+
+}  // namespace gslm
+
+namespace gslm {
+int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, int64_t N,
+                      const float* dL_dcolor, const float* dL_dinv, const ScratchBufs& sb, hipStream_t s);
+int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, const BinBufs& bb,
+                          const ScratchBufs& sb, const GradK& out, bool want_means, hipStream_t s);
+int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
+                       const ScratchBufs& sb, hipStream_t s);
+int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
+               const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
+               hipStream_t s);
+int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
+                         const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s);
+}  // namespace gslm

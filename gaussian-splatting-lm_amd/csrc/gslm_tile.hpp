@@ -1,0 +1,169 @@
+// gslm_tile.hpp -- per-tile front-to-back (JVP) and back-to-front (VJP) passes shared by the
+// drop-in backward, the drop-in jvp and the fused LM matvec kernels.
+//
+// VJP accumulation strategy (MI355X-specific): instead of upstream's per-pixel global atomicAdd
+// (10 atomics per pixel-Gaussian pair), every wave reduces a Gaussian's per-pixel contributions
+// with a 6-step DPP reduction, the 4 waves' partials meet in LDS, and each (tile, Gaussian) pair
+// writes ONE 48-B row with plain coalesced stores into its slot of the sorted list.  The
+// per-Gaussian sum over tiles is done later by a gather in the preprocess-backward kernel.
+// No float atomics anywhere: results are bitwise reproducible run to run.
+#pragma once
+#include "gslm_kernels.hpp"
+
+namespace gslm {
+
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, BANK_MASK, true));
+}
+
+// Sum over the 64 lanes of a wave; the total lands in lane 63.  Requires all 64 lanes active.
+__device__ __forceinline__ float wave_sum_lane63(float x) {
+  x += dpp_f<0x111>(x);       // row_shr:1
+  x += dpp_f<0x112>(x);       // row_shr:2
+  x += dpp_f<0x114>(x);       // row_shr:4
+  x += dpp_f<0x118>(x);       // row_shr:8   -> lane 15 of each row holds the row sum
+  x += dpp_f<0x142, 0xa>(x);  // row_bcast:15 into rows 1 and 3
+  x += dpp_f<0x143, 0xc>(x);  // row_bcast:31 into rows 2 and 3 -> lane 63 holds the total
+  return x;
+}
+
+// Contribution row layout (12 floats = 3 float4) per (tile, Gaussian) slot of the sorted list:
+//   [0] dL/dx_pix [1] dL/dy_pix [2] dL/dconic.a [3] dL/dconic.b [4] dL/dconic.c [5] dL/dopacity_eff
+//   [6..8] dL/drgb  [9] dL/dinvdepth  [10..11] 0
+constexpr int NV = 10;
+
+struct VjpPix {
+  float T;          // running transmittance (starts at final_T)
+  float T_final;
+  uint32_t last;    // n_contrib (1-based index of the last blended Gaussian)
+  float dpix[3];    // dL/dcolor of this pixel
+  float dinv;       // dL/dinvdepth of this pixel
+  float bg_dot;     // <bg, dL/dpix>
+  float acc[3], acc_inv, last_alpha, last_color[3], last_inv;
+};
+
+__device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside, float T_final, uint32_t last,
+                                         float d0, float d1, float d2, float dinv) {
+  s.T_final = inside ? T_final : 0.f;
+  s.T = s.T_final;
+  s.last = inside ? last : 0u;
+  s.dpix[0] = d0; s.dpix[1] = d1; s.dpix[2] = d2;
+  s.dinv = dinv;
+  s.bg_dot = (v.bg[0] * d0 + v.bg[1] * d1) + v.bg[2] * d2;
+  s.acc[0] = s.acc[1] = s.acc[2] = 0.f;
+  s.acc_inv = 0.f;
+  s.last_alpha = 0.f;
+  s.last_color[0] = s.last_color[1] = s.last_color[2] = 0.f;
+  s.last_inv = 0.f;
+}
+
+// Back-to-front pass over the tile's list (upstream BACKWARD::renderCUDA semantics), writing one
+// reduced row per list slot into contrib.  Block-uniform control flow; requires blockDim = 256.
+// WITH_XY: compute dL/dxy; WITH_INV: propagate dL/dinvdepth.
+template <bool WITH_XY, bool WITH_INV>
+__device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, uint2 range,
+                                         const uint32_t* __restrict__ point_list, const float4* __restrict__ rec,
+                                         float4* s_r0, float4* s_r1, float4* s_r2, float* s_acc, int* s_misc,
+                                         float4* __restrict__ contrib) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // Positions >= max over pixels of n_contrib are never blended: write zero rows for them.
+  if (tid == 0) s_misc[0] = 0;
+  __syncthreads();
+  if (st.last) atomicMax(&s_misc[0], (int)st.last);
+  __syncthreads();
+  const int n_eff = s_misc[0];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t k = (int64_t)range.x + n_eff + tid; k < (int64_t)range.y; k += TILE_PIX) {
+    contrib[3 * k + 0] = z4;
+    contrib[3 * k + 1] = z4;
+    contrib[3 * k + 2] = z4;
+  }
+  const int rounds = (n_eff + TILE_PIX - 1) / TILE_PIX;
+  uint32_t contributor = (uint32_t)n_eff;
+  for (int r = 0; r < rounds; ++r) {
+    const int base = n_eff - 1 - r * TILE_PIX;  // list position of batch element 0
+    const int cnt = min(TILE_PIX, base + 1);
+    __syncthreads();
+    if (tid < cnt) {
+      const uint32_t g = point_list[range.x + base - tid];
+      s_r0[tid] = rec[3 * (int64_t)g + 0];
+      s_r1[tid] = rec[3 * (int64_t)g + 1];
+      s_r2[tid] = rec[3 * (int64_t)g + 2];
+    }
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      --contributor;
+      const float4 a = s_r0[j];
+      const float4 b = s_r1[j];
+      const float4 c = s_r2[j];
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float G = expf(power);
+      const float alpha = fminf(0.99f, b.y * G);
+      const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
+      float gv[NV];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) gv[q] = 0.f;
+      if (valid) {
+        st.T = st.T / (1.f - alpha);
+        const float dchannel = alpha * st.T;
+        const float col[3] = {b.z, b.w, c.x};
+        float dL_dalpha = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          st.acc[ch] = st.last_alpha * st.last_color[ch] + (1.f - st.last_alpha) * st.acc[ch];
+          st.last_color[ch] = col[ch];
+          dL_dalpha += (col[ch] - st.acc[ch]) * st.dpix[ch];
+          gv[6 + ch] = dchannel * st.dpix[ch];
+        }
+        if (WITH_INV) {
+          const float invd = c.y;
+          st.acc_inv = st.last_alpha * st.last_inv + (1.f - st.last_alpha) * st.acc_inv;
+          st.last_inv = invd;
+          dL_dalpha += (invd - st.acc_inv) * st.dinv;
+          gv[9] = dchannel * st.dinv;
+        }
+        dL_dalpha *= st.T;
+        st.last_alpha = alpha;
+        dL_dalpha += (-st.T_final / (1.f - alpha)) * st.bg_dot;
+        const float dL_dG = b.y * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        if (WITH_XY) {
+          gv[0] = dL_dG * (-gdx * a.z - gdy * a.w);
+          gv[1] = dL_dG * (-gdy * b.x - gdx * a.w);
+        }
+        gv[2] = -0.5f * gdx * dx * dL_dG;
+        gv[3] = -gdx * dy * dL_dG;
+        gv[4] = -0.5f * gdy * dy * dL_dG;
+        gv[5] = G * dL_dalpha;
+      }
+      const bool any = __ballot(valid) != 0ull;
+      if (any) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+          if ((q < 2 && !WITH_XY) || (q == 9 && !WITH_INV)) continue;
+          gv[q] = wave_sum_lane63(gv[q]);
+        }
+      }
+      if (lane == 63) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) s_acc[(w * NV + q) * TILE_PIX + j] = any ? gv[q] : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tid < cnt) {
+      float t[NV];
+#pragma unroll
+      for (int q = 0; q < NV; ++q)
+        t[q] = ((s_acc[(0 * NV + q) * TILE_PIX + tid] + s_acc[(1 * NV + q) * TILE_PIX + tid]) +
+                s_acc[(2 * NV + q) * TILE_PIX + tid]) + s_acc[(3 * NV + q) * TILE_PIX + tid];
+      const int64_t k = (int64_t)range.x + base - tid;
+      contrib[3 * k + 0] = make_float4(t[0], t[1], t[2], t[3]);
+      contrib[3 * k + 1] = make_float4(t[4], t[5], t[6], t[7]);
+      contrib[3 * k + 2] = make_float4(t[8], t[9], 0.f, 0.f);
+    }
+  }
+}
+
+}  // namespace gslm

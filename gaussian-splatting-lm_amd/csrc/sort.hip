@@ -1,0 +1,241 @@
+// sort.hip -- stable LSD radix sort of (u32 key, u32 value) pairs and an exclusive u32 scan.
+//
+// Replaces cub::DeviceRadixSort::SortPairs / cub::DeviceScan::InclusiveSum of the upstream
+// rasterizer_impl (SURVEY §2 kernel table).  Written for wave64: the stable in-block ranking uses
+// 8 wave ballots per digit (a "match" of equal digits), per-wave digit counts in LDS and a
+// 4-wave prefix, so every block scatters its 4096 keys in input order (stability is what keeps
+// depth ties in Gaussian-index order).
+//
+// Per pass: hist (read keys) -> per-digit scan over blocks -> scatter (read keys+vals, write both).
+#include "gslm_internal.hpp"
+
+namespace gslm {
+
+namespace {
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// Block-wide inclusive scan for 256 threads.  Returns inclusive value; *total = block sum.
+__device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w, uint32_t* total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t inc = wave_incl_scan(x, lane);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t v = s_w[k];
+    if (k < w) off += v;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return inc + off;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n,
+                                                             int shift, uint32_t* __restrict__ hist,
+                                                             int nblocks) {
+  __shared__ uint32_t cnt[RADIX];
+  const int tid = threadIdx.x;
+  cnt[tid] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+#pragma unroll 4
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const int64_t i = base + r * SORT_THREADS + tid;
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (RADIX - 1)], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)tid * nblocks + blockIdx.x] = cnt[tid];
+}
+
+// One block per digit: exclusive scan of that digit's per-block counts; digit total -> totals[d].
+__global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int nblocks,
+                                                    uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_w[4];
+  const int d = blockIdx.x, tid = threadIdx.x;
+  uint32_t* h = hist + (int64_t)d * nblocks;
+  uint32_t carry = 0;
+  for (int base = 0; base < nblocks; base += 256) {
+    const int i = base + tid;
+    const uint32_t x = i < nblocks ? h[i] : 0u;
+    uint32_t tot;
+    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
+    if (i < nblocks) h[i] = carry + inc - x;
+    carry += tot;
+  }
+  if (tid == 0) totals[d] = carry;
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+    uint32_t* __restrict__ vout, int64_t n, int shift, const uint32_t* __restrict__ hist, int nblocks,
+    const uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_base[RADIX];
+  __shared__ uint32_t s_wc[4][RADIX];
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+
+  // issue all loads first (16 keys + 16 values per thread in flight)
+  uint32_t key[SORT_ITEMS], val[SORT_ITEMS];
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const int64_t i = base + r * SORT_THREADS + tid;
+    key[r] = i < n ? kin[i] : 0u;
+    val[r] = i < n ? vin[i] : 0u;
+  }
+
+  // digit base for this block = exclusive prefix of digit totals + this block's offset
+  {
+    const uint32_t t = totals[tid];
+    uint32_t tot;
+    const uint32_t inc = block_incl_scan256(t, s_w, &tot);
+    s_base[tid] = inc - t + hist[(int64_t)tid * nblocks + blockIdx.x];
+  }
+  __syncthreads();
+
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const int64_t i = base + r * SORT_THREADS + tid;
+    const bool valid = i < n;
+    const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_wc[w][lane + 64 * k] = 0u;
+    unsigned long long m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = __popcll(m & lt_mask);
+    if (valid && rank == 0) s_wc[w][d] = (uint32_t)__popcll(m);
+    __syncthreads();
+    {
+      const uint32_t c0 = s_wc[0][tid], c1 = s_wc[1][tid], c2 = s_wc[2][tid], c3 = s_wc[3][tid];
+      const uint32_t b0 = s_base[tid];
+      s_wc[0][tid] = b0;
+      s_wc[1][tid] = b0 + c0;
+      s_wc[2][tid] = b0 + c0 + c1;
+      s_wc[3][tid] = b0 + c0 + c1 + c2;
+      s_base[tid] = b0 + c0 + c1 + c2 + c3;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = s_wc[w][d] + rank;
+      kout[pos] = key[r];
+      vout[pos] = val[r];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------- scan ----------------
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* __restrict__ in,
+                                                              const uint32_t* __restrict__ idx, int64_t n,
+                                                              uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) acc += in[idx ? idx[i] : i];
+  }
+  uint32_t tot;
+  block_incl_scan256(acc, s_w, &tot);
+  if (tid == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ block_sums, int nb,
+                                                  uint32_t* __restrict__ total) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  uint32_t carry = 0;
+  for (int base = 0; base < nb; base += 256) {
+    const int i = base + tid;
+    const uint32_t x = i < nb ? block_sums[i] : 0u;
+    uint32_t tot;
+    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
+    if (i < nb) block_sums[i] = carry + inc - x;
+    carry += tot;
+  }
+  if (tid == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __restrict__ in,
+                                                             const uint32_t* __restrict__ idx, int64_t n,
+                                                             const uint32_t* __restrict__ block_sums,
+                                                             uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    v[k] = i < n ? in[idx ? idx[i] : i] : 0u;
+    acc += v[k];
+  }
+  uint32_t tot;
+  const uint32_t inc = block_incl_scan256(acc, s_w, &tot);
+  uint32_t run = block_sums[blockIdx.x] + inc - acc;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+}
+
+}  // namespace
+
+int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s) {
+  *result_in_alt = false;
+  if (n <= 0) return GSLM_OK;
+  const int nb = (int)sort_blocks(n);
+  uint32_t* totals = hist + (size_t)RADIX * nb;
+  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+  bool alt = false;
+  for (int shift = 0; shift < end_bit; shift += 8) {
+    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, hist, nb);
+    hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vi, ko, vo, n, shift, hist,
+                       nb, totals);
+    GSLM_LAUNCH_CHECK();
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+    alt = !alt;
+  }
+  *result_in_alt = alt;
+  return GSLM_OK;
+}
+
+int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
+                       uint32_t* total, hipStream_t s) {
+  if (n <= 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(total, 0, 4, s));
+    return GSLM_OK;
+  }
+  const int nb = (int)scan_blocks(n);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, tmp, nb, total);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+}  // namespace gslm

@@ -1,0 +1,210 @@
+"""ctypes binding of libgslm.so (C ABI in include/gslm.h).
+
+There is deliberately no fallback: if the HIP library is missing the import fails loudly, so no
+caller can silently run a CPU or eager-PyTorch path in its place.
+"""
+import ctypes
+import math
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSLM_LIB", os.path.join(os.path.dirname(_HERE), "build", "libgslm.so"))
+
+GSLM_OK = 0
+GSLM_ERR_INVALID = -1
+GSLM_ERR_HIP = -2
+GSLM_ERR_CAPACITY = -3
+
+
+class GslmView(ctypes.Structure):
+    _fields_ = [
+        ("image_height", ctypes.c_int32), ("image_width", ctypes.c_int32),
+        ("tanfovx", ctypes.c_double), ("tanfovy", ctypes.c_double), ("scale_modifier", ctypes.c_double),
+        ("viewmatrix", ctypes.c_float * 16), ("projmatrix", ctypes.c_float * 16),
+        ("campos", ctypes.c_float * 3), ("bg", ctypes.c_float * 3),
+        ("sh_degree", ctypes.c_int32), ("prefiltered", ctypes.c_int32),
+        ("antialiasing", ctypes.c_int32), ("debug", ctypes.c_int32),
+    ]
+
+
+class GslmGaussians(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int64), ("max_coeffs", ctypes.c_int32), ("raw", ctypes.c_int32),
+        ("means3D", ctypes.c_void_p), ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
+        ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
+        ("sh_dc", ctypes.c_void_p), ("sh_dc_stride", ctypes.c_int64),
+        ("sh_rest", ctypes.c_void_p), ("sh_rest_stride", ctypes.c_int64),
+        ("colors_precomp", ctypes.c_void_p),
+    ]
+
+
+class GslmGrads(ctypes.Structure):
+    _fields_ = [
+        ("means2D", ctypes.c_void_p), ("means3D", ctypes.c_void_p), ("opacities", ctypes.c_void_p),
+        ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p), ("cov3D", ctypes.c_void_p),
+        ("sh_dc", ctypes.c_void_p), ("sh_dc_stride", ctypes.c_int64),
+        ("sh_rest", ctypes.c_void_p), ("sh_rest_stride", ctypes.c_int64),
+        ("colors", ctypes.c_void_p), ("accumulate", ctypes.c_int32),
+    ]
+
+
+# Every symbol include/gslm.h declares; tests check the library exports each of them.
+EXPORTS = {
+    "gslm_geom_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "gslm_image_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "gslm_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "gslm_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]),
+    "gslm_preprocess": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_num_rendered": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.c_void_p]),
+    "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_forward": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
+                                    ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                    ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "gslm_backward": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.POINTER(GslmGrads), ctypes.c_void_p]),
+    "gslm_jvp": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
+                                ctypes.POINTER(GslmGaussians), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_matvec_view": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
+                                        ctypes.POINTER(GslmGrads), ctypes.c_void_p, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
+                                        ctypes.c_void_p]),
+    "gslm_dot_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "gslm_dot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_axpy_dev": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_xpby_dev": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_damp_add": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p]),
+    "gslm_inspect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p]),
+    "gslm_last_error": (ctypes.c_char_p, []),
+    "gslm_abi_version": (ctypes.c_int, []),
+}
+
+
+class GslmError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libgslm.so not found at {LIB_PATH}: build it with "
+                          f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (restype, argtypes) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    return lib
+
+
+lib = _load()
+
+
+def check(status, what=""):
+    if status != GSLM_OK:
+        msg = lib.gslm_last_error().decode(errors="replace")
+        raise GslmError(f"{what or 'gslm'} failed ({status}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL).  Tensors must be fp32/int32 contiguous."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _host_floats(t, n):
+    if isinstance(t, torch.Tensor):
+        return [float(x) for x in t.detach().reshape(-1).to("cpu", torch.float32).tolist()][:n]
+    return [float(x) for x in list(t)][:n]
+
+
+def make_view(H, W, tanfovx, tanfovy, bg, scale_modifier, viewmatrix, projmatrix, sh_degree, campos,
+              prefiltered=False, antialiasing=False, debug=False):
+    v = GslmView()
+    v.image_height, v.image_width = int(H), int(W)
+    v.tanfovx, v.tanfovy, v.scale_modifier = float(tanfovx), float(tanfovy), float(scale_modifier)
+    v.viewmatrix[:] = _host_floats(viewmatrix, 16)
+    v.projmatrix[:] = _host_floats(projmatrix, 16)
+    v.campos[:] = _host_floats(campos, 3)
+    v.bg[:] = _host_floats(bg, 3)
+    v.sh_degree = int(sh_degree)
+    v.prefiltered, v.antialiasing, v.debug = int(bool(prefiltered)), int(bool(antialiasing)), int(bool(debug))
+    return v
+
+
+def view_from_settings(s):
+    """GaussianRasterizationSettings -> GslmView (gaussian_renderer/__init__.py:36-50 field names)."""
+    return make_view(s.image_height, s.image_width, s.tanfovx, s.tanfovy, s.bg, s.scale_modifier,
+                     s.viewmatrix, s.projmatrix, s.sh_degree, s.campos, s.prefiltered, s.antialiasing, s.debug)
+
+
+def view_from_camera(cam, bg, sh_degree, scale_modifier=1.0, antialiasing=False):
+    """The settings render() builds from a Camera (gaussian_renderer/__init__.py:33-50)."""
+    return make_view(cam.image_height, cam.image_width, math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
+                     bg, scale_modifier, cam.world_view_transform, cam.full_proj_transform, sh_degree,
+                     cam.camera_center, antialiasing=antialiasing)
+
+
+def make_gaussians(P, means3D=None, opacities=None, scales=None, rotations=None, cov3D=None, sh_dc=None,
+                   sh_dc_stride=0, sh_rest=None, sh_rest_stride=0, max_coeffs=1, colors=None, raw=False):
+    g = GslmGaussians()
+    g.P = int(P)
+    g.max_coeffs = int(max_coeffs)
+    g.raw = int(bool(raw))
+    g.means3D, g.opacities, g.scales = ptr(means3D), ptr(opacities), ptr(scales)
+    g.rotations, g.cov3D_precomp = ptr(rotations), ptr(cov3D)
+    g.sh_dc, g.sh_dc_stride = sh_dc, int(sh_dc_stride)
+    g.sh_rest, g.sh_rest_stride = sh_rest, int(sh_rest_stride)
+    g.colors_precomp = ptr(colors)
+    return g
+
+
+def sh_pointers(shs=None, dc=None, rest=None):
+    """(dc_ptr, dc_stride, rest_ptr, rest_stride, K) for a [P,K,3] shs tensor or a (dc, rest) pair."""
+    if shs is not None:
+        K = shs.shape[1]
+        base = shs.data_ptr()
+        return base, 3 * K, (base + 12 if K > 1 else None), 3 * K, K
+    if dc is not None:
+        K = 1 + (rest.shape[1] if rest is not None else 0)
+        return dc.data_ptr(), 3, (rest.data_ptr() if rest is not None and K > 1 else None), 3 * (K - 1), K
+    return None, 0, None, 0, 1
+
+
+def make_grads(means2D=None, means3D=None, opacities=None, scales=None, rotations=None, cov3D=None,
+               sh=None, dc=None, rest=None, colors=None, accumulate=False):
+    g = GslmGrads()
+    g.means2D, g.means3D, g.opacities = ptr(means2D), ptr(means3D), ptr(opacities)
+    g.scales, g.rotations, g.cov3D, g.colors = ptr(scales), ptr(rotations), ptr(cov3D), ptr(colors)
+    dcp, dcs, rp, rs, _ = sh_pointers(sh, dc, rest)
+    g.sh_dc, g.sh_dc_stride, g.sh_rest, g.sh_rest_stride = dcp, dcs, rp, rs
+    g.accumulate = int(bool(accumulate))
+    return g
+
+
+def u8(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)

@@ -1,0 +1,178 @@
+/*
+ * gslm.h -- C ABI of the MI355X-native Gaussian-splat rasterizer + LM normal-equations matvec.
+ *
+ * Drop-in boundary.  The reference binds its rasterizer through pybind11
+ * (`diff_gaussian_rasterization._C`, absent submodule) from the Python call sites below; every
+ * entry point here replaces one of those calls:
+ *
+ *   gslm_preprocess + gslm_rasterize (= gslm_forward)
+ *        <- GaussianRasterizer.forward, called at gaussian_renderer/__init__.py:102-110,
+ *           gaussian_renderer/batch_render.py:100-108, gaussian_renderer/reference_render.py:102
+ *   gslm_backward   <- autograd backward of the rasterizer, driven by loss_image_state.py:93-97
+ *                      from solver/solver_functions.py:119 (matvec_T)
+ *   gslm_jvp        <- forward-mode tangent of the rasterizer (fork), driven by fwAD at
+ *                      solver/solver_functions.py:86-92 (matvec)
+ *   gslm_matvec_view<- fused (J^T W J) v of one view: solver_functions.py:83-132 matvec followed
+ *                      by matvec_T with the disable_ssim residual of batch_training_loss.py:10-17
+ *   gslm_cg_*       <- GaussianModelState dot / saxpy (solver/gaussian_model_state.py:197-273)
+ *                      used by cgls_damped (solver/conjugate_gradient.py:51-127), device resident
+ *
+ * Conventions: raw device pointers, sizes, a settings POD and a hipStream_t (passed as void*).
+ * Every function returns GSLM_OK (0) or a negative status; gslm_last_error() describes the last
+ * failure.  No internal threads, no allocation (the caller allocates workspaces sized by the
+ * *_bytes queries), stream ordered, not re-entrant on one workspace.  Only gslm_num_rendered and
+ * gslm_forward (which calls it) synchronise the stream (the upstream forward does the same to
+ * size its binning buffers).
+ */
+#ifndef GSLM_H
+#define GSLM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSLM_OK 0
+#define GSLM_ERR_INVALID (-1)
+#define GSLM_ERR_HIP (-2)
+#define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
+
+#define GSLM_ABI_VERSION 1
+
+/* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
+typedef struct gslm_view {
+  int32_t image_height;
+  int32_t image_width;
+  double tanfovx;
+  double tanfovy;
+  double scale_modifier;
+  float viewmatrix[16]; /* world_view_transform, row-major torch storage (= column-major for the kernel) */
+  float projmatrix[16]; /* full_proj_transform */
+  float campos[3];
+  float bg[3];
+  int32_t sh_degree;    /* active SH degree D */
+  int32_t prefiltered;
+  int32_t antialiasing;
+  int32_t debug;
+} gslm_view;
+
+/* Per-Gaussian inputs.  With raw = 0 they are the activated tensors the rasterizer receives
+ * (means3D, opacities = sigmoid, scales = exp, rotations = normalize, shs = cat(dc, rest));
+ * with raw = 1 they are the GaussianModel leaves (_xyz, _opacity, _scaling, _rotation,
+ * _features_dc, _features_rest, scene/gaussian_model.py:53-69) and the activations of
+ * gaussian_model.py:192-220 are fused into the kernels.  SH coefficient k of Gaussian i,
+ * channel c is sh_dc[i*sh_dc_stride + c] for k = 0 and sh_rest[i*sh_rest_stride + 3*(k-1) + c]
+ * otherwise.  For tangents (gslm_jvp) the same struct carries the tangent tensors; a NULL pointer
+ * means a zero tangent. */
+typedef struct gslm_gaussians {
+  int64_t P;
+  int32_t max_coeffs; /* K: coefficients stored per Gaussian (dc + rest) */
+  int32_t raw;
+  const float* means3D;       /* [P,3] */
+  const float* opacities;     /* [P]   */
+  const float* scales;        /* [P,3] or NULL when cov3D_precomp is given */
+  const float* rotations;     /* [P,4] (w,x,y,z) */
+  const float* cov3D_precomp; /* [P,6] or NULL */
+  const float* sh_dc;         /* or NULL when colors_precomp is given */
+  int64_t sh_dc_stride;
+  const float* sh_rest;
+  int64_t sh_rest_stride;
+  const float* colors_precomp; /* [P,3] or NULL */
+} gslm_gaussians;
+
+/* Gradients / param-space vectors, one pointer per GaussianModelState group
+ * (solver/gaussian_model_state.py:52-62).  NULL = not requested.  Strides as in gslm_gaussians. */
+typedef struct gslm_grads {
+  float* means2D;   /* [P,3] NDC-space screen gradient (means2D.grad, gaussian_model.py:561-563) */
+  float* means3D;   /* [P,3] */
+  float* opacities; /* [P]   */
+  float* scales;    /* [P,3] */
+  float* rotations; /* [P,4] */
+  float* cov3D;     /* [P,6] (only when cov3D_precomp was the input) */
+  float* sh_dc;
+  int64_t sh_dc_stride;
+  float* sh_rest;
+  int64_t sh_rest_stride;
+  float* colors;    /* [P,3] (only when colors_precomp was the input) */
+  int32_t accumulate; /* 1: add into the outputs, 0: overwrite */
+} gslm_grads;
+
+/* ---- workspace sizing (two-call protocol: query, allocate with the caller's allocator, call) ---- */
+size_t gslm_geom_bytes(int64_t P);
+size_t gslm_image_bytes(int32_t H, int32_t W);
+size_t gslm_binning_bytes(int64_t num_rendered, int32_t H, int32_t W);
+size_t gslm_scratch_bytes(int64_t P, int64_t num_rendered); /* backward / jvp / matvec scratch */
+
+/* ---- forward (rasterizer_impl forward: preprocess -> scan -> duplicateWithKeys -> sort -> ranges -> render) ---- */
+/* Per-Gaussian preprocess, depth sort and tile-count scan.  Writes radii (int32 [P]) if non-NULL. */
+int gslm_preprocess(const gslm_view* view, const gslm_gaussians* g, void* geom, size_t geom_bytes,
+                    int32_t* out_radii, void* stream);
+/* Synchronous read of the number of (tile, Gaussian) pairs produced by gslm_preprocess. */
+int gslm_num_rendered(const void* geom, int64_t P, int64_t* out_num_rendered, void* stream);
+/* Binning + tile sort + ranges + per-tile blend.  out_color [3,H,W], out_invdepth [1,H,W] (nullable). */
+int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                   int64_t num_rendered, void* image, size_t image_bytes, float* out_color,
+                   float* out_invdepth, void* stream);
+/* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
+ * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
+ * gslm_rasterize with a larger buffer). */
+int gslm_forward(const gslm_view* view, const gslm_gaussians* g, void* geom, size_t geom_bytes,
+                 void* binning, size_t binning_bytes, void* image, size_t image_bytes,
+                 float* out_color, float* out_invdepth, int32_t* out_radii,
+                 int64_t* out_num_rendered, void* stream);
+
+/* ---- backward (VJP) of gslm_forward.  dL_dinvdepth may be NULL. ---- */
+int gslm_backward(const gslm_view* view, const gslm_gaussians* g, const void* geom, const void* binning,
+                  int64_t num_rendered, const void* image, const float* dL_dcolor,
+                  const float* dL_dinvdepth, void* scratch, size_t scratch_bytes,
+                  const gslm_grads* out, void* stream);
+
+/* ---- forward-mode tangent (JVP) of gslm_forward; reuses the forward's sorted lists.
+ * means2D_tangent [P,3] may be NULL. ---- */
+int gslm_jvp(const gslm_view* view, const gslm_gaussians* g, const gslm_gaussians* tangent,
+             const float* means2D_tangent, const void* geom, const void* binning, int64_t num_rendered,
+             const void* image, void* scratch, size_t scratch_bytes, float* out_color_t,
+             float* out_invdepth_t, void* stream);
+
+/* ---- fused LM normal-equations product of one view:
+ *   y += 2 * J^T ( w (.) (J v) )     (J: d clamp-free render / d raw params, g->raw must be 1)
+ * w [3,H,W] is the per-pixel weight m^2 * 1[0 <= R <= 1] of the disable_ssim residual
+ * (batch_training_loss.py:10-17; the factor 2 is the [r; r] aliasing).
+ * mask_xyz = 1 freezes the xyz group (train_jvp.py:221-227): v.xyz is ignored, y.xyz untouched. ---- */
+int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
+                     const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
+                     int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
+                     const gslm_grads* y, void* stream);
+
+/* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
+ * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
+size_t gslm_dot_scratch_bytes(int64_t n);
+/* out (double, device) = sum_i a_i b_i d_i  (d = NULL means 1).  Deterministic. */
+int gslm_dot(const float* a, const float* b, const int64_t* group_bounds, const double* group_damp,
+             int32_t ngroups, int64_t n, void* scratch, double* out_dev, void* stream);
+/* y = alpha * x + y, alpha read from device memory as num/den (den==NULL -> 1), times sign. */
+int gslm_axpy_dev(int64_t n, const double* num_dev, const double* den_dev, float sign, const float* x,
+                  float* y, void* stream);
+/* p = s + beta p, beta = num/den from device memory */
+int gslm_xpby_dev(int64_t n, const float* s, const double* num_dev, const double* den_dev, float* p,
+                  void* stream);
+/* y += d[group] * x (the damping term D x) */
+int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const double* group_damp,
+                  int32_t ngroups, float* y, void* stream);
+
+/* ---- diagnostics: device-to-device copies of internal buffers (any output may be NULL) ----
+ * point_list [N] u32 (Gaussian id per sorted slot), ranges [ntiles*2] u32, tiles_touched [P] u32,
+ * final_T [H*W] f32, n_contrib [H*W] u32, render records [P*12] f32. */
+int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t num_rendered, int32_t H, int32_t W,
+                 const void* image, uint32_t* point_list, uint32_t* ranges, uint32_t* tiles_touched,
+                 float* final_T, uint32_t* n_contrib, float* records, void* stream);
+
+const char* gslm_last_error(void);
+int gslm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSLM_H */
