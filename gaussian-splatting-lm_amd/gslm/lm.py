@@ -1,0 +1,266 @@
+"""Matrix-free Levenberg-Marquardt on the HIP rasterizer: the hot path of train_jvp.py's LM branch.
+
+Reference semantics:
+  * residual (batch_training_loss.py:10-17, disable_ssim=True):  r_b = m_b * clamp01(R_b) - gt_b, and
+    the "ssim" slot aliases r, so the residual vector is [r; r]: loss = 2 ||r||^2, J^T J = 2 J_r^T J_r.
+  * cgls_damped (conjugate_gradient.py:51-127) solves (J^T J + D) x = J^T b with b = -[r; r]
+    (train_jvp.py:243), D the per-group diagonal of GaussianModelDampMatrix (train_jvp.py:229-235),
+    xyz frozen by the param mask (train_jvp.py:221-227).
+  * line search: alpha = 2, 1, ..., 1/16 on the validation views, keep the best (train_jvp.py:264-279).
+
+MI355X design: the operator A = J^T J + D is applied by one fused HIP pass per view (gslm_matvec_view:
+tangent preprocess -> JVP tile pass -> weight -> VJP tile pass -> gather-sum preprocess backward) on
+geometry cached once per LM step (the sort is not redone per matvec).  CG runs on flat param-space
+vectors with its scalars in device memory (gslm_dot / gslm_axpy_dev / gslm_xpby_dev): with
+`check=False` an iteration has no host synchronisation at all.  CGLS on (J, D) and CG on A generate
+the same iterates in exact arithmetic; the reference's restart schedule and stopping tests are kept.
+"""
+import ctypes
+import math
+
+import torch
+
+from gslm import _lib
+from gslm._lib import check, lib
+from gslm.params import GROUPS, ParamLayout, raw_gaussians
+
+# train_jvp.py:229-235
+DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
+                "opacity": 5e-2, "exposure": 1e1}
+
+
+class ViewRaster:
+    """Primal forward of one view on raw GaussianModel leaves + the buffers the matvec reuses."""
+
+    def __init__(self, view, device):
+        self.view = view
+        self.H, self.W = view.image_height, view.image_width
+        self.device = device
+        self.N = 0
+        self.geom = self.binning = self.image = self.scratch = None
+
+    def forward(self, g, stream):
+        P = g.P
+        dev = self.device
+        if self.geom is None or self.geom.numel() < lib.gslm_geom_bytes(P):
+            self.geom = _lib.u8(lib.gslm_geom_bytes(P), dev)
+            self.image = _lib.u8(lib.gslm_image_bytes(self.H, self.W), dev)
+            self.color = torch.empty(3, self.H, self.W, dtype=torch.float32, device=dev)
+            self.invdepth = torch.empty(1, self.H, self.W, dtype=torch.float32, device=dev)
+            self.radii = torch.empty(P, dtype=torch.int32, device=dev)
+        check(lib.gslm_preprocess(ctypes.byref(self.view), ctypes.byref(g), self.geom.data_ptr(), self.geom.numel(),
+                                  self.radii.data_ptr(), stream), "gslm_preprocess")
+        n = ctypes.c_int64(0)
+        check(lib.gslm_num_rendered(self.geom.data_ptr(), P, ctypes.byref(n), stream), "gslm_num_rendered")
+        self.N = int(n.value)
+        need = lib.gslm_binning_bytes(self.N, self.H, self.W)
+        if self.binning is None or self.binning.numel() < need:
+            self.binning = _lib.u8(int(need * 1.25) + 4096, dev)
+        check(lib.gslm_rasterize(ctypes.byref(self.view), P, self.geom.data_ptr(), self.binning.data_ptr(),
+                                 self.binning.numel(), self.N, self.image.data_ptr(), self.image.numel(),
+                                 self.color.data_ptr(), self.invdepth.data_ptr(), stream), "gslm_rasterize")
+        need = lib.gslm_scratch_bytes(P, self.N)
+        if self.scratch is None or self.scratch.numel() < need:
+            self.scratch = _lib.u8(int(need * 1.25) + 4096, dev)
+        return self.color
+
+
+class LMProblem:
+    """The LM normal equations of one camera batch (one LM step's worth of cached geometry)."""
+
+    def __init__(self, model, cams, bg, gts=None, alpha_masks=None, mask_xyz=True, damp=None, device="cuda"):
+        self.model = model
+        self.cams = cams
+        self.device = device
+        self.bg = bg
+        self.mask_xyz = bool(mask_xyz)
+        P = model._xyz.shape[0]
+        K = 1 + model._features_rest.shape[1]
+        self.layout = ParamLayout(P, K, model._exposure.shape[0])
+        self.damp = DEFAULT_DAMP if damp is None else damp
+        self._bounds, self._damps = self.layout.group_damp_arrays(self.damp)
+        self.gts = [c.original_image.to(device) for c in cams] if gts is None else gts
+        self.masks = [c.alpha_mask.to(device) for c in cams] if alpha_masks is None else alpha_masks
+        self.views = [ViewRaster(_lib.view_from_camera(c, bg, model.active_sh_degree), device) for c in cams]
+        self.stream = _lib.stream_handle(device)
+        self.dot_scratch = torch.empty(lib.gslm_dot_scratch_bytes(0) // 8 + 8, dtype=torch.float64, device=device)
+        self.weights = [None] * len(cams)
+        self.residuals = [None] * len(cams)
+
+    # -------------------------------------------------------------- residual (A8)
+    def evaluate(self):
+        """Primal forward of every view; residuals, per-pixel weights, loss = 2 sum ||r||^2 (device)."""
+        g = raw_gaussians(self.model)
+        loss = torch.zeros((), dtype=torch.float64, device=self.device)
+        for b, vr in enumerate(self.views):
+            R = vr.forward(g, self.stream)
+            m = self.masks[b]
+            inside = ((R >= 0) & (R <= 1)).to(torch.float32)
+            r = m * R.clamp(0, 1) - self.gts[b]
+            self.residuals[b] = r
+            self.weights[b] = (m * m * inside).contiguous()
+            loss += 2.0 * (r.double() * r.double()).sum()
+        self.loss = loss
+        return loss
+
+    def num_rendered(self):
+        return [v.N for v in self.views]
+
+    # -------------------------------------------------------------- J^T b
+    def rhs(self, out):
+        """out = J^T b = -2 sum_b J_b^T (m (.) 1[0<=R<=1] (.) r_b) in the flat layout (xyz, exposure zeroed)."""
+        out.zero_()
+        g = raw_gaussians(self.model)
+        grads = self.layout.grads_struct(out, accumulate=True)
+        for b, vr in enumerate(self.views):
+            m = self.masks[b]
+            R = vr.color
+            inside = ((R >= 0) & (R <= 1)).to(torch.float32)
+            dL = (-2.0 * m * inside * self.residuals[b]).contiguous()
+            check(lib.gslm_backward(ctypes.byref(vr.view), ctypes.byref(g), vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                    vr.N, vr.image.data_ptr(), dL.data_ptr(), None, vr.scratch.data_ptr(),
+                                    vr.scratch.numel(), ctypes.byref(grads), self.stream), "gslm_backward")
+        self._apply_mask(out)
+        return out
+
+    def _apply_mask(self, vec):
+        o = self.layout.offsets
+        if self.mask_xyz:
+            vec[o["xyz"][0]:o["xyz"][1]].zero_()
+        vec[o["exposure"][0]:o["exposure"][1]].zero_()
+
+    # -------------------------------------------------------------- (J^T J + D) v
+    def matvec(self, v, y):
+        """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view)."""
+        y.zero_()
+        g = raw_gaussians(self.model)
+        vs = self.layout.grads_struct(v)
+        ys = self.layout.grads_struct(y, accumulate=True)
+        for b, vr in enumerate(self.views):
+            check(lib.gslm_matvec_view(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                       self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
+                                       vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
+                                       vr.scratch.numel(), ctypes.byref(ys), self.stream), "gslm_matvec_view")
+        self.damp_add(v, y)
+        return y
+
+    def damp_add(self, v, y):
+        check(lib.gslm_damp_add(v.numel(), v.data_ptr(), self._bounds, self._damps, 7, y.data_ptr(), self.stream))
+
+    # -------------------------------------------------------------- device scalar algebra
+    def dot(self, a, b, out_slot, damped=False):
+        if damped:
+            check(lib.gslm_dot(a.data_ptr(), b.data_ptr(), self._bounds, self._damps, 7, a.numel(),
+                               self.dot_scratch.data_ptr(), out_slot, self.stream))
+        else:
+            check(lib.gslm_dot(a.data_ptr(), b.data_ptr(), None, None, 0, a.numel(), self.dot_scratch.data_ptr(),
+                               out_slot, self.stream))
+
+    def zeros(self):
+        return torch.zeros(self.layout.numel, dtype=torch.float32, device=self.device)
+
+
+def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check_every=True, verbose=False,
+               callback=None):
+    """cgls_damped (conjugate_gradient.py:51-127) on the fused operator, x0 = 0.
+
+    Returns (x, info).  With check_every=False the stopping tests are skipped and no iteration
+    synchronises with the host (benchmark mode); the iterates are identical either way while no
+    test fires."""
+    n = prob.layout.numel
+    dev = prob.device
+    st = prob.stream
+    sc = torch.zeros(16, dtype=torch.float64, device=dev)
+    ptr = lambda i: sc.data_ptr() + 8 * i
+    GAM, DEL, GAMN, XG, XS = 0, 1, 2, 3, 4
+    x = torch.zeros(n, dtype=torch.float32, device=dev)
+    s = torch.empty_like(x)
+    p = torch.empty_like(x)
+    q = torch.empty_like(x)
+    b2 = float(prob.loss) if check_every else None  # ||b||^2 = loss
+    iter_total, last_res, history = 0, math.inf, []
+    first = True
+    while iter_total < max_iter:
+        if first:
+            s.copy_(g)  # s0 = J^T b - D x0 with x0 = 0
+            first = False
+        else:
+            prob.matvec(x, q)
+            torch.sub(g, q, out=s)
+        p.copy_(s)
+        prob.dot(s, s, ptr(GAM))
+        stop = False
+        for _ in range(restart_iter):
+            prob.matvec(p, q)
+            prob.dot(p, q, ptr(DEL))
+            if check_every and sc[DEL].item() < 1e-20:
+                if verbose:
+                    print("Early termination: delta is too small.")
+                stop = True
+                break
+            check(lib.gslm_axpy_dev(n, ptr(GAM), ptr(DEL), 1.0, p.data_ptr(), x.data_ptr(), st))
+            check(lib.gslm_axpy_dev(n, ptr(GAM), ptr(DEL), -1.0, q.data_ptr(), s.data_ptr(), st))
+            prob.dot(s, s, ptr(GAMN))
+            check(lib.gslm_xpby_dev(n, s.data_ptr(), ptr(GAMN), ptr(GAM), p.data_ptr(), st))
+            if check_every:
+                prob.dot(x, g, ptr(XG))
+                prob.dot(x, s, ptr(XS))
+                vals = sc[:5].tolist()
+                res = b2 - vals[XG] - vals[XS]  # ||b - J x||^2 + x^T D x  (monitor of conjugate_gradient.py:103-104)
+                history.append(res)
+                if verbose:
+                    print(f"[Iter {iter_total + 1}] res: {res:.2e}")
+                if res > last_res:
+                    stop = True
+                    break
+                last_res = res
+                if vals[GAMN] < max(tol * math.sqrt(vals[GAM]), atol):
+                    stop = True
+                    break
+            if callback is not None:
+                callback(x, s, iter_total + 1)
+            sc[GAM].copy_(sc[GAMN])
+            iter_total += 1
+            if iter_total >= max_iter:
+                stop = True
+                break
+        if stop:
+            break
+    return x, {"iters": iter_total, "residuals": history}
+
+
+def update_params(model, layout, step, scale):
+    """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step."""
+    v = layout.views(step)
+    with torch.no_grad():
+        model._xyz.add_(v["xyz"], alpha=scale)
+        model._features_dc.add_(v["features_dc"], alpha=scale)
+        model._features_rest.add_(v["features_rest"], alpha=scale)
+        model._scaling.add_(v["scaling"], alpha=scale)
+        model._rotation.add_(v["rotation"], alpha=scale)
+        model._opacity.add_(v["opacity"], alpha=scale)
+        model._exposure.add_(v["exposure"], alpha=scale)
+
+
+def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
+            verbose=False, device="cuda"):
+    """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search."""
+    prob = LMProblem(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
+    start_loss = prob.evaluate()
+    g = prob.rhs(prob.zeros())
+    s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
+                         verbose=verbose)
+    val = LMProblem(model, val_cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
+    alpha = 2.0
+    best_alpha, best_loss = alpha, math.inf
+    update_params(model, prob.layout, s, alpha)
+    for _ in range(6):
+        vl = float(val.evaluate())
+        if vl < best_loss:
+            best_loss, best_alpha = vl, alpha
+        new_alpha = alpha * 0.5
+        update_params(model, prob.layout, s, new_alpha - alpha)
+        alpha = new_alpha
+    update_params(model, prob.layout, s, best_alpha - alpha)
+    final = float(val.evaluate())
+    return dict(start_loss=float(start_loss), final_val_loss=final, best_alpha=best_alpha, cg=info, step=s)
