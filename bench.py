@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""bench.py -- CG matvecs/s + raster Mpix/s of the MI355X LM hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the 1-GPU LM config; configs[3] at N = 8): P = 1M synthetic
+Gaussians, SH degree 3, one 1920x1080 view per GPU (views sharded, weak scaling), random-init
+model / seeded cameras / GT = render of a perturbed copy (SURVEY §8(d) recipe; no datasets here).
+
+One step = one CG iteration of the LM solve: the fused (J^T J + D) p over the whole view batch
+(per view: tangent preprocess -> fused JVP->VJP tile pass -> gather-sum backward; then one RCCL
+all-reduce of the param-space vector when N > 1) plus the CG vector updates, device resident.
+The primal forward / sort is done once per LM step (outside the timed region, reported as
+raster Mpix/s from a separate timed loop of full forwards).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-lm_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "CG matvecs/sec + raster Mpix/s, 1M Gaussians @1080p, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--sh", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--views-per-gpu", type=int, default=1)
+    ap.add_argument("--s0", type=float, default=0.005)
+    ap.add_argument("--cpu-tiles", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--forward-steps", type=int, default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    from gslm import _lib
+    from gslm.cameras import orbit_cameras
+    from gslm.lm import LMProblem, cgls_fused
+    from gslm.model import synthetic_gaussians
+    from gslm.parallel import ShardedLMProblem, shard_views
+
+    n_views = world_size * args.views_per_gpu
+    W, H = args.width, args.height
+    cams_all = orbit_cameras(n_views, W, H, seed=1)
+    mine = shard_views(n_views, rank, world_size)
+    cams = [cams_all[i] for i in mine]
+    bg = torch.zeros(3)
+
+    # GT (seed 2): render of the model with f_dc / opacity / scaling perturbed by N(0, 0.01^2)
+    pert = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views)
+    g2 = torch.Generator().manual_seed(2)
+    with torch.no_grad():
+        pert._features_dc += 0.01 * torch.randn(pert._features_dc.shape, generator=g2)
+        pert._opacity += 0.01 * torch.randn(pert._opacity.shape, generator=g2)
+        pert._scaling += 0.01 * torch.randn(pert._scaling.shape, generator=g2)
+    pert.to(device)
+    gt_prob = LMProblem(pert, [c.to(device) for c in cams], bg, device=device)
+    gt_prob.evaluate()
+    for c, vr in zip(cams, gt_prob.views):
+        c.original_image = vr.color.clamp(0, 1).clone()
+    del gt_prob, pert
+
+    model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
+    prob = ShardedLMProblem(model, cams, bg, device=device)
+    prob.evaluate()
+    g = prob.rhs(prob.zeros())
+    torch.cuda.synchronize()
+    n_rendered = prob.num_rendered()
+
+    def barrier():
+        if world_size > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world_size > 1:
+            t = torch.tensor([x], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        return x
+
+    # ---------------- timed: K CG iterations (fused matvec + vector ops), no host sync inside
+    cgls_fused(prob, g, max_iter=max(args.warmup, 1), restart_iter=max(args.warmup, 1), check_every=False)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    x, _ = cgls_fused(prob, g, max_iter=args.steps, restart_iter=args.steps, check_every=False)
+    torch.cuda.synchronize()
+    barrier()
+    t_cg = max_over_ranks(time.perf_counter() - t0)
+    ms_per_step = 1e3 * t_cg / args.steps
+
+    # ---------------- raster Mpix/s: full forwards (preprocess, sort, binning, blend; includes the
+    # num_rendered read-back the upstream forward also does)
+    fsteps = args.forward_steps or args.steps
+    from gslm.params import raw_gaussians
+    graw = raw_gaussians(model)
+    for vr in prob.views:
+        vr.forward(graw, prob.stream)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(fsteps):
+        for vr in prob.views:
+            vr.forward(graw, prob.stream)
+    torch.cuda.synchronize()
+    barrier()
+    t_fwd = max_over_ranks(time.perf_counter() - t0)
+    mpix = n_views * W * H * fsteps / t_fwd / 1e6
+
+    # ---------------- roofline of the dominant kernel: the fused JVP->VJP tile pass (k_render_matvec)
+    vr = prob.views[0]
+    vs = prob.layout.grads_struct(x)
+    ys = prob.layout.grads_struct(prob.zeros(), accumulate=True)
+    lib, check = _lib.lib, _lib.check
+
+    def stage(mask):
+        check(lib.gslm_matvec_view_stages(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
+                                          prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                          vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                          ctypes.byref(ys), mask, prob.stream))
+
+    stage(1)
+    stage(2)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = max(args.steps, 5)
+    ev0.record()
+    for _ in range(reps):
+        stage(2)
+    ev1.record()
+    torch.cuda.synchronize()
+    render_ms = ev0.elapsed_time(ev1) / reps
+    # per-stage times (tangent, gather) for the breakdown
+    def time_stage(mask, n=reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            stage(mask)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+    tangent_ms = time_stage(1)
+    gather_ms = time_stage(4)
+    N0, HW = vr.N, W * H
+    # algorithmic bytes of one k_render_matvec launch (SURVEY §8(d) per-unit figures):
+    #   per (tile, Gaussian) entry: JVP pass primal gather 44 + tangent gather 40,
+    #   VJP pass primal gather 44 + one gradient row 40 (plain store, replaces the atomic RMW)
+    #   per pixel: n_contrib 4 + final_T 4 + weight 12
+    alg_bytes = 168 * N0 + 20 * HW
+    achieved = alg_bytes / (render_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_render_matvec.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pm = json.load(f)
+            if pm.get("P") == args.P and pm.get("width") == W and pm.get("height") == H:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        from oracle.cpu_baseline import cpu_matvec_rate
+        cm = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu")
+        cc = orbit_cameras(1, W, H, seed=1)[0]
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+        r = cpu_matvec_rate(cm, cc, torch.zeros(3), n_tiles=args.cpu_tiles, repeats=2, threads=threads)
+        cpu = {"value": 1.0 / r["matvec_s"], "unit": "view-matvec/s", "cores": r["threads"], "kind": "port",
+               "sample": (f"oracle/torch_raster.py (PyTorch CPU, {r['threads']} threads, {r['cpu_model']}): "
+                          f"all {args.P} Gaussians through preprocess+binning with forward-AD and autograd, "
+                          f"blend JVP+VJP on {r['n_tiles']} of {r['ntiles']} tiles spread over the 1080p frame, "
+                          f"scaled to the full frame; t_pre={r['t_pre']:.2f}s t_sub={r['t_sub']:.2f}s"),
+               "raster_mpix_s": W * H / r["forward_s"] / 1e6}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": n_views * args.steps / t_cg,
+            "unit": "view-matvec/s (one (J^T J + D) application per 1080p view, 1M Gaussians)",
+            "n_gpus": world_size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded Gaussians / orbit cameras / GT = render of perturbed model)",
+            "config": {"workload": f"LM CG iteration, {args.P} Gaussians SH{args.sh}, {args.views_per_gpu}x{W}x{H} "
+                                   f"view(s) per GPU (BASELINE configs[2]; configs[3] at 8 GPUs)",
+                       "P": args.P, "sh_degree": args.sh, "width": W, "height": H,
+                       "views_total": n_views, "parallelism": f"views sharded x{world_size}"},
+            "cg_matvecs_per_s": args.steps / t_cg,
+            "raster_mpix_s": mpix,
+            "forward_ms_per_view": 1e3 * t_fwd / fsteps / max(len(prob.views), 1),
+            "num_rendered": n_rendered,
+            "stage_ms": {"tangent_preprocess": tangent_ms, "render_matvec": render_ms, "gather_backward": gather_ms},
+            "roofline": {"bound": "hbm", "kernel": "k_render_matvec", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -315,23 +315,33 @@ int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussia
                     (hipStream_t)stream);
 }
 
-int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
-                     const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning, int64_t N,
-                     const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y, void* stream) {
+int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
+                            const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
+                            int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
+                            int32_t stages, void* stream) {
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;
   if (!vin || !y || !pixel_weight) { set_error("matvec: NULL argument"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
-  if ((st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, s))) return st;
-  if (N > 0 && (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s))) return st;
+  if ((stages & GSLM_STAGE_TANGENT) && (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, s))) return st;
+  if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
+      (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
+    return st;
   GradK yk = make_gradk(y);
   yk.accumulate = 1;
   yk.means2D = nullptr;
   if (mask_xyz) yk.means3D = nullptr;
-  if (N == 0) return GSLM_OK;
+  if (N == 0 || !(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
   return launch_preprocess_bwd(b.v, b.g, b.gb, b.bb, b.sb, yk, mask_xyz == 0, s);
+}
+
+int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
+                     const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning, int64_t N,
+                     const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y, void* stream) {
+  return gslm_matvec_view_stages(view, gi, vin, pixel_weight, mask_xyz, geom, binning, N, image, scratch,
+                                 scratch_bytes, y, GSLM_STAGE_ALL, stream);
 }
 
 int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, int32_t H, int32_t W,

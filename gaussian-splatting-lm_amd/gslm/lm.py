@@ -133,6 +133,12 @@ class LMProblem:
     def matvec(self, v, y):
         """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view)."""
         y.zero_()
+        self.local_normal_matvec(v, y)
+        self.damp_add(v, y)
+        return y
+
+    def local_normal_matvec(self, v, y):
+        """y += sum over this problem's views of 2 J_b^T W_b J_b v (no damping)."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
         ys = self.layout.grads_struct(y, accumulate=True)
@@ -141,7 +147,6 @@ class LMProblem:
                                        self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
                                        vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
                                        vr.scratch.numel(), ctypes.byref(ys), self.stream), "gslm_matvec_view")
-        self.damp_add(v, y)
         return y
 
     def damp_add(self, v, y):

@@ -146,6 +146,18 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
                      int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
                      const gslm_grads* y, void* stream);
 
+/* The three stages of gslm_matvec_view, separately launchable (profiling, overlap):
+ * TANGENT: per-Gaussian tangent records from v; RENDER: fused JVP->VJP tile pass writing one row per
+ * (tile, Gaussian); GATHER: per-Gaussian gather-sum + chain rule, y += ... */
+#define GSLM_STAGE_TANGENT 1
+#define GSLM_STAGE_RENDER 2
+#define GSLM_STAGE_GATHER 4
+#define GSLM_STAGE_ALL 7
+int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
+                            const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
+                            int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
+                            const gslm_grads* y, int32_t stages, void* stream);
+
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
 size_t gslm_dot_scratch_bytes(int64_t n);

@@ -196,19 +196,19 @@ def binning(pre):
     Returns (point_list[int64], tile_of_entry[int64], ranges[num_tiles, 2])."""
     gx, gy = pre["grid"]
     vis = np.nonzero(pre["visible"].numpy())[0]
-    rect = pre["rect"].numpy()
+    rect = pre["rect"].numpy()[vis]
     depth_bits = pre["depth"].detach().to(torch.float32).numpy().view(np.uint32)
-    tiles, gids, dkeys = [], [], []
-    for g in vis:
-        x0, y0, x1, y1 = rect[g]
-        for ty in range(y0, y1):
-            for tx in range(x0, x1):
-                tiles.append(ty * gx + tx)
-                gids.append(g)
-                dkeys.append(depth_bits[g])
-    tiles = np.asarray(tiles, dtype=np.int64)
-    gids = np.asarray(gids, dtype=np.int64)
-    dkeys = np.asarray(dkeys, dtype=np.uint64)
+    x0, y0, x1, y1 = rect[:, 0], rect[:, 1], rect[:, 2], rect[:, 3]
+    nx = x1 - x0
+    cnt = nx * (y1 - y0)
+    total = int(cnt.sum())
+    # duplicateWithKeys in row-major rect order (vectorised)
+    gids = np.repeat(vis.astype(np.int64), cnt)
+    start = np.repeat(np.cumsum(cnt) - cnt, cnt)
+    local = np.arange(total, dtype=np.int64) - start
+    nxr = np.repeat(nx, cnt)
+    tiles = (np.repeat(y0, cnt) + local // np.maximum(nxr, 1)) * gx + np.repeat(x0, cnt) + local % np.maximum(nxr, 1)
+    dkeys = depth_bits[gids].astype(np.uint64)
     # stable radix sort of the 64-bit key with input in Gaussian-index order == lexsort by (tile, depth, index)
     order = np.lexsort((gids, dkeys, tiles)) if len(tiles) else np.zeros(0, dtype=np.int64)
     point_list = gids[order]
@@ -221,7 +221,7 @@ def binning(pre):
     return torch.from_numpy(point_list), torch.from_numpy(tile_sorted), torch.from_numpy(ranges)
 
 
-def blend(pre, point_list, ranges, H, W, bg):
+def blend(pre, point_list, ranges, H, W, bg, tile_subset=None):
     """Per-tile front-to-back alpha blending (App. A step 11), dense per tile.
     Returns color[3,H,W], invdepth[1,H,W], final_T[H,W], n_contrib[H,W] (int32)."""
     gx, gy = pre["grid"]
@@ -240,7 +240,7 @@ def blend(pre, point_list, ranges, H, W, bg):
             pix_chunks.append(py * W + px)
             s, e = int(ranges[t, 0]), int(ranges[t, 1])
             npx = py.numel()
-            if e <= s:
+            if e <= s or (tile_subset is not None and t not in tile_subset):
                 col_chunks.append(bg[None, :].expand(npx, 3) * torch.ones(npx, 1, dtype=dtype))
                 dep_chunks.append(torch.zeros(npx, dtype=dtype))
                 T_chunks.append(torch.ones(npx, dtype=dtype))
