@@ -145,7 +145,7 @@ def main():
         check(lib.gslm_matvec_view_stages(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
                                           prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
-                                          ctypes.byref(ys), mask, prob.stream))
+                                          ctypes.byref(ys), mask, None, prob.stream))
 
     stage(1)
     stage(2)

@@ -40,7 +40,7 @@ size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
   g.keys_alt = c.take<uint32_t>(P);
   g.vals_alt = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
-  g.offset_by_g = c.take<uint32_t>(P);
+  g.goff = c.take<uint32_t>(P);
   g.hist = c.take<uint32_t>(sort_hist_bytes(P) / 4);
   g.scan_tmp = c.take<uint32_t>(scan_tmp_bytes(P) / 4);
   g.counters = c.take<uint32_t>(16);
@@ -55,11 +55,13 @@ size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
   b.keys1 = c.take<uint32_t>(N);
   b.vals0 = c.take<uint32_t>(N);
   b.vals1 = c.take<uint32_t>(N);
-  b.gid = c.take<uint32_t>(N);
-  b.point_list = c.take<uint32_t>(N);
-  b.inv = c.take<uint32_t>(N);
   b.hist = c.take<uint32_t>(sort_hist_bytes(N) / 4);
   b.ranges = c.take<uint2>(ntiles);
+  b.end_bit = 1;
+  while ((1ll << b.end_bit) < (long long)ntiles) ++b.end_bit;
+  b.passes = (b.end_bit + 7) / 8;
+  b.point_list = (b.passes & 1) ? b.vals1 : b.vals0;
+  b.keys_sorted = (b.passes & 1) ? b.keys1 : b.keys0;
   if (o) *o = b;
   return c.off;
 }
@@ -147,6 +149,7 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
   st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s);
   if (st) return st;
   if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  if ((st = exclusive_scan_u32(gb.tiles, nullptr, gb.goff, P, gb.scan_tmp, gb.counters + 1, s))) return st;
   return exclusive_scan_u32(gb.tiles, gb.sorted_idx, gb.offsets, P, gb.scan_tmp, gb.counters, s);
 }
 
@@ -318,30 +321,28 @@ int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussia
 int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
                             const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                             int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
-                            int32_t stages, void* stream) {
+                            int32_t stages, const double* damp7, void* stream) {
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;
   if (!vin || !y || !pixel_weight) { set_error("matvec: NULL argument"); return GSLM_ERR_INVALID; }
+  if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
   if ((stages & GSLM_STAGE_TANGENT) && (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, s))) return st;
   if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
       (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
     return st;
-  GradK yk = make_gradk(y);
-  yk.accumulate = 1;
-  yk.means2D = nullptr;
-  if (mask_xyz) yk.means3D = nullptr;
-  if (N == 0 || !(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
-  return launch_preprocess_bwd(b.v, b.g, b.gb, b.bb, b.sb, yk, mask_xyz == 0, s);
+  if (!(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
+  return launch_gather_lm(b.v, b.g, b.gb, b.sb, make_gradk(y), make_gradk(vin), damp7,
+                          (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, s);
 }
 
 int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
                      const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning, int64_t N,
                      const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y, void* stream) {
   return gslm_matvec_view_stages(view, gi, vin, pixel_weight, mask_xyz, geom, binning, N, image, scratch,
-                                 scratch_bytes, y, GSLM_STAGE_ALL, stream);
+                                 scratch_bytes, y, GSLM_STAGE_ALL, nullptr, stream);
 }
 
 int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, int32_t H, int32_t W,

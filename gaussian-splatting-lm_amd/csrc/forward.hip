@@ -43,35 +43,22 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                     const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ tiles,
-                                                    const uint2* __restrict__ rect, uint32_t* __restrict__ offset_by_g,
-                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                    uint32_t* __restrict__ gid) {
+                                                    const uint2* __restrict__ rect, uint32_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= P) return;
   const uint32_t g = sorted_idx[s];
   const uint32_t n = tiles[g];
-  uint32_t off = offsets[s];
-  offset_by_g[g] = off;
   if (n == 0) return;
+  uint32_t off = offsets[s];
   const uint2 rc = rect[g];
   const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
   for (int ty = y0; ty < y1; ++ty)
     for (int tx = x0; tx < x1; ++tx) {
       keys[off] = (uint32_t)(ty * gx + tx);
-      vals[off] = off;
-      gid[off] = g;
+      vals[off] = g;
       ++off;
     }
-}
-
-__global__ __launch_bounds__(256) void k_finalize(int64_t N, const uint32_t* __restrict__ sorted_dup,
-                                                   const uint32_t* __restrict__ gid,
-                                                   uint32_t* __restrict__ point_list, uint32_t* __restrict__ inv) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= N) return;
-  const uint32_t d = sorted_dup[k];
-  point_list[k] = gid[d];
-  inv[d] = (uint32_t)k;
 }
 
 __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __restrict__ keys,
@@ -172,20 +159,18 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0)
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
-                       gb.offsets, gb.tiles, gb.rect, gb.offset_by_g, bb.keys0, bb.vals0, bb.gid);
+                       gb.offsets, gb.tiles, gb.rect, bb.keys0, bb.vals0);
   GSLM_LAUNCH_CHECK();
   if (N == 0) return GSLM_OK;
-  int end_bit = 0;
-  while ((1ll << end_bit) < (long long)ntiles) ++end_bit;
-  if (end_bit == 0) end_bit = 1;
   bool alt = false;
-  int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, end_bit, bb.hist, &alt, s);
+  int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s);
   if (st != GSLM_OK) return st;
-  const uint32_t* skeys = alt ? bb.keys1 : bb.keys0;
-  const uint32_t* svals = alt ? bb.vals1 : bb.vals0;
+  if ((alt ? bb.vals1 : bb.vals0) != bb.point_list) {
+    set_error("internal: radix pass count disagrees with the binning layout");
+    return GSLM_ERR_INVALID;
+  }
   const unsigned nbN = (unsigned)((N + 255) / 256);
-  hipLaunchKernelGGL(k_finalize, dim3(nbN), dim3(256), 0, s, N, svals, bb.gid, bb.point_list, bb.inv);
-  hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, skeys, bb.ranges);
+  hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -148,23 +148,33 @@ struct GeomBufs {
   uint32_t* keys_alt;     // [P]
   uint32_t* vals_alt;     // [P]
   uint32_t* vals_init;    // [P] identity
-  uint32_t* offsets;      // [P] exclusive scan of tiles in depth order
-  uint32_t* offset_by_g;  // [P] dup start of Gaussian g
+  uint32_t* offsets;      // [P] exclusive scan of tiles in depth order (duplicate emission)
+  uint32_t* goff;         // [P] exclusive scan of tiles in Gaussian-index order (gradient-row slots)
   uint32_t* hist;         // radix histogram
   uint32_t* scan_tmp;     // scan block sums
-  uint32_t* counters;     // [0] = num_rendered
+  uint32_t* counters;     // [0] = num_rendered, [1] = sum of tiles (== [0])
 };
+// Binning: (tile id, Gaussian id) pairs emitted in depth order, stably sorted by tile id.
+// The number of radix passes (hence which ping-pong buffer holds the result) depends only on the
+// tile count, so every consumer derives the same point_list / keys_sorted pointers.
 struct BinBufs {
   uint32_t* keys0;
   uint32_t* keys1;
   uint32_t* vals0;
   uint32_t* vals1;
-  uint32_t* gid;
-  uint32_t* point_list;
-  uint32_t* inv;
+  uint32_t* point_list;   // sorted Gaussian ids (aliases vals0 or vals1)
+  uint32_t* keys_sorted;  // sorted tile ids (aliases keys0 or keys1)
   uint32_t* hist;
   uint2* ranges;
+  int passes;
+  int end_bit;
 };
+// Gradient rows: one row per (Gaussian, touched tile), at slot goff[g] + (ty - ymin) * nx + (tx - xmin),
+// i.e. grouped by Gaussian index so the per-Gaussian sum reads contiguous memory.
+__device__ __forceinline__ uint32_t row_slot(uint32_t goff_g, uint2 rc, int tx, int ty) {
+  const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
+  return goff_g + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+}
 struct ImgBufs {
   float* final_T;
   uint32_t* n_contrib;
@@ -198,4 +208,6 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
                hipStream_t s);
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
                          const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s);
+int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
+                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, hipStream_t s);
 }  // namespace gslm

@@ -1,12 +1,12 @@
-// gslm_tile.hpp -- per-tile front-to-back (JVP) and back-to-front (VJP) passes shared by the
-// drop-in backward, the drop-in jvp and the fused LM matvec kernels.
+// gslm_tile.hpp -- per-tile back-to-front (VJP) pass shared by the drop-in backward and the fused
+// LM matvec kernels.
 //
 // VJP accumulation strategy (MI355X-specific): instead of upstream's per-pixel global atomicAdd
 // (10 atomics per pixel-Gaussian pair), every wave reduces a Gaussian's per-pixel contributions
 // with a 6-step DPP reduction, the 4 waves' partials meet in LDS, and each (tile, Gaussian) pair
-// writes ONE 48-B row with plain coalesced stores into its slot of the sorted list.  The
-// per-Gaussian sum over tiles is done later by a gather in the preprocess-backward kernel.
-// No float atomics anywhere: results are bitwise reproducible run to run.
+// writes ONE row with plain stores.  Rows are grouped by Gaussian index (row_slot), so the
+// per-Gaussian sum over tiles in the gather kernel reads contiguous memory.  No float atomics
+// anywhere: results are bitwise reproducible run to run.
 #pragma once
 #include "gslm_kernels.hpp"
 
@@ -28,10 +28,52 @@ __device__ __forceinline__ float wave_sum_lane63(float x) {
   return x;
 }
 
-// Contribution row layout (12 floats = 3 float4) per (tile, Gaussian) slot of the sorted list:
-//   [0] dL/dx_pix [1] dL/dy_pix [2] dL/dconic.a [3] dL/dconic.b [4] dL/dconic.c [5] dL/dopacity_eff
-//   [6..8] dL/drgb  [9] dL/dinvdepth  [10..11] 0
+// Screen-space gradient of one (tile, Gaussian) pair, value index q:
+//   0 dL/dx_pix  1 dL/dy_pix  2 dL/dconic.a  3 dL/dconic.b  4 dL/dconic.c  5 dL/dopacity_eff
+//   6..8 dL/drgb  9 dL/dinvdepth
+// Row formats: ROWF4 = 3 (general): [x y a b | c o r g | b inv 0 0]
+//              ROWF4 = 2 (LM, xyz frozen, no depth term): [a b c o | r g b 0]
 constexpr int NV = 10;
+
+template <bool WITH_XY, bool WITH_INV>
+__host__ __device__ constexpr bool q_used(int q) {
+  return (q >= 2 && q <= 8) || (q < 2 && WITH_XY) || (q == 9 && WITH_INV);
+}
+template <bool WITH_XY, bool WITH_INV>
+__host__ __device__ constexpr int n_used() {
+  return 7 + (WITH_XY ? 2 : 0) + (WITH_INV ? 1 : 0);
+}
+template <bool WITH_XY, bool WITH_INV>
+__host__ __device__ constexpr int q_slot(int q) {
+  int s = 0;
+  for (int k = 0; k < q; ++k) s += q_used<WITH_XY, WITH_INV>(k) ? 1 : 0;
+  return s;
+}
+
+template <int ROWF4>
+__device__ __forceinline__ void store_row(float4* __restrict__ rows, uint32_t slot, const float t[NV]) {
+  if (ROWF4 == 3) {
+    rows[3 * (size_t)slot + 0] = make_float4(t[0], t[1], t[2], t[3]);
+    rows[3 * (size_t)slot + 1] = make_float4(t[4], t[5], t[6], t[7]);
+    rows[3 * (size_t)slot + 2] = make_float4(t[8], t[9], 0.f, 0.f);
+  } else {
+    rows[2 * (size_t)slot + 0] = make_float4(t[2], t[3], t[4], t[5]);
+    rows[2 * (size_t)slot + 1] = make_float4(t[6], t[7], t[8], 0.f);
+  }
+}
+
+template <int ROWF4>
+__device__ __forceinline__ void load_row(const float4* __restrict__ rows, size_t slot, float t[NV]) {
+  if (ROWF4 == 3) {
+    const float4 a = rows[3 * slot + 0], b = rows[3 * slot + 1], c = rows[3 * slot + 2];
+    t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w; t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
+    t[8] = c.x; t[9] = c.y;
+  } else {
+    const float4 a = rows[2 * slot + 0], b = rows[2 * slot + 1];
+    t[0] = 0.f; t[1] = 0.f; t[2] = a.x; t[3] = a.y; t[4] = a.z; t[5] = a.w; t[6] = b.x; t[7] = b.y;
+    t[8] = b.z; t[9] = 0.f;
+  }
+}
 
 struct VjpPix {
   float T;          // running transmittance (starts at final_T)
@@ -58,26 +100,34 @@ __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside,
   s.last_inv = 0.f;
 }
 
-// Back-to-front pass over the tile's list (upstream BACKWARD::renderCUDA semantics), writing one
-// reduced row per list slot into contrib.  Block-uniform control flow; requires blockDim = 256.
-// WITH_XY: compute dL/dxy; WITH_INV: propagate dL/dinvdepth.
+// LDS floats needed by vjp_tile's per-wave partial sums
 template <bool WITH_XY, bool WITH_INV>
-__device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, uint2 range,
-                                         const uint32_t* __restrict__ point_list, const float4* __restrict__ rec,
-                                         float4* s_r0, float4* s_r1, float4* s_r2, float* s_acc, int* s_misc,
-                                         float4* __restrict__ contrib) {
+constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * TILE_PIX; }
+
+// Back-to-front pass over the tile's list (upstream BACKWARD::renderCUDA semantics), writing one
+// reduced row per (tile, Gaussian) pair.  Block-uniform control flow; requires blockDim = 256.
+template <bool WITH_XY, bool WITH_INV, int ROWF4>
+__device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, int tile_x, int tile_y,
+                                         uint2 range, const uint32_t* __restrict__ point_list,
+                                         const float4* __restrict__ rec, const uint2* __restrict__ rect,
+                                         const uint32_t* __restrict__ goff, float4* s_r0, float4* s_r1,
+                                         float4* s_r2, float* s_acc, int* s_misc, float4* __restrict__ rows) {
+  constexpr int NU = n_used<WITH_XY, WITH_INV>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // Positions >= max over pixels of n_contrib are never blended: write zero rows for them.
+  // Positions >= max over pixels of n_contrib are never blended: their rows are zero.
   if (tid == 0) s_misc[0] = 0;
   __syncthreads();
   if (st.last) atomicMax(&s_misc[0], (int)st.last);
   __syncthreads();
   const int n_eff = s_misc[0];
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t k = (int64_t)range.x + n_eff + tid; k < (int64_t)range.y; k += TILE_PIX) {
-    contrib[3 * k + 0] = z4;
-    contrib[3 * k + 1] = z4;
-    contrib[3 * k + 2] = z4;
+  {
+    float z[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) z[q] = 0.f;
+    for (int64_t k = (int64_t)range.x + n_eff + tid; k < (int64_t)range.y; k += TILE_PIX) {
+      const uint32_t g = point_list[k];
+      store_row<ROWF4>(rows, row_slot(goff[g], rect[g], tile_x, tile_y), z);
+    }
   }
   const int rounds = (n_eff + TILE_PIX - 1) / TILE_PIX;
   uint32_t contributor = (uint32_t)n_eff;
@@ -85,11 +135,13 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     const int base = n_eff - 1 - r * TILE_PIX;  // list position of batch element 0
     const int cnt = min(TILE_PIX, base + 1);
     __syncthreads();
+    uint32_t my_slot = 0;
     if (tid < cnt) {
       const uint32_t g = point_list[range.x + base - tid];
       s_r0[tid] = rec[3 * (int64_t)g + 0];
       s_r1[tid] = rec[3 * (int64_t)g + 1];
       s_r2[tid] = rec[3 * (int64_t)g + 2];
+      my_slot = row_slot(goff[g], rect[g], tile_x, tile_y);
     }
     __syncthreads();
     for (int j = 0; j < cnt; ++j) {
@@ -141,27 +193,29 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       const bool any = __ballot(valid) != 0ull;
       if (any) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) {
-          if ((q < 2 && !WITH_XY) || (q == 9 && !WITH_INV)) continue;
-          gv[q] = wave_sum_lane63(gv[q]);
-        }
+        for (int q = 0; q < NV; ++q)
+          if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
       }
       if (lane == 63) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) s_acc[(w * NV + q) * TILE_PIX + j] = any ? gv[q] : 0.f;
+        for (int q = 0; q < NV; ++q)
+          if (q_used<WITH_XY, WITH_INV>(q))
+            s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
       }
     }
     __syncthreads();
     if (tid < cnt) {
       float t[NV];
 #pragma unroll
-      for (int q = 0; q < NV; ++q)
-        t[q] = ((s_acc[(0 * NV + q) * TILE_PIX + tid] + s_acc[(1 * NV + q) * TILE_PIX + tid]) +
-                s_acc[(2 * NV + q) * TILE_PIX + tid]) + s_acc[(3 * NV + q) * TILE_PIX + tid];
-      const int64_t k = (int64_t)range.x + base - tid;
-      contrib[3 * k + 0] = make_float4(t[0], t[1], t[2], t[3]);
-      contrib[3 * k + 1] = make_float4(t[4], t[5], t[6], t[7]);
-      contrib[3 * k + 2] = make_float4(t[8], t[9], 0.f, 0.f);
+      for (int q = 0; q < NV; ++q) {
+        t[q] = 0.f;
+        if (q_used<WITH_XY, WITH_INV>(q)) {
+          const int sq = q_slot<WITH_XY, WITH_INV>(q);
+          t[q] = ((s_acc[(0 * NU + sq) * TILE_PIX + tid] + s_acc[(1 * NU + sq) * TILE_PIX + tid]) +
+                  s_acc[(2 * NU + sq) * TILE_PIX + tid]) + s_acc[(3 * NU + sq) * TILE_PIX + tid];
+        }
+      }
+      store_row<ROWF4>(rows, my_slot, t);
     }
   }
 }

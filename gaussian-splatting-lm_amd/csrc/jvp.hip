@@ -131,12 +131,14 @@ template <bool WITH_XY>
 __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __restrict__ ranges,
                                                         const uint32_t* __restrict__ point_list,
                                                         const float4* __restrict__ rec, const float4* __restrict__ trec,
+                                                        const uint2* __restrict__ rect,
+                                                        const uint32_t* __restrict__ goff,
                                                         const float* __restrict__ final_T,
                                                         const uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ weight, float4* __restrict__ contrib) {
   __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_r2[TILE_PIX];
   __shared__ float4 s_t0[TILE_PIX], s_t1[TILE_PIX], s_t2[TILE_PIX];
-  __shared__ float s_acc[4 * NV * TILE_PIX];
+  __shared__ float s_acc[vjp_acc_floats<WITH_XY, false>()];
   __shared__ int s_misc[4];
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -164,8 +166,8 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   const float u2 = 2.f * w2 * (o.dC[2] + o.dT * v.bg[2]);
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
-  vjp_tile<WITH_XY, false>(st, inside, (float)px, (float)py, range, point_list, rec, s_r0, s_r1, s_r2, s_acc, s_misc,
-                           contrib);
+  vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
+                                            rect, goff, s_r0, s_r1, s_r2, s_acc, s_misc, contrib);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -203,10 +205,10 @@ int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, co
   const int ntiles = v.gx * v.gy;
   if (mask_xyz)
     hipLaunchKernelGGL(k_render_matvec<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
-                       gb.rec, sb.trec, ib.final_T, ib.n_contrib, weight, sb.contrib);
+                       gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
   else
     hipLaunchKernelGGL(k_render_matvec<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
-                       gb.rec, sb.trec, ib.final_T, ib.n_contrib, weight, sb.contrib);
+                       gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

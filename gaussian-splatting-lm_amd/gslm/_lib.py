@@ -84,7 +84,7 @@ EXPORTS = {
                                                ctypes.POINTER(GslmGrads), ctypes.c_void_p, ctypes.c_int32,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
-                                               ctypes.c_int32, ctypes.c_void_p]),
+                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p]),
     "gslm_dot_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gslm_dot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                 ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,

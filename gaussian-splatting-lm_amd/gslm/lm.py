@@ -25,6 +25,9 @@ from gslm._lib import check, lib
 from gslm.params import GROUPS, ParamLayout, raw_gaussians
 
 # train_jvp.py:229-235
+STAGE_ALL = 7
+STAGE_OVERWRITE = 8
+
 DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
                 "opacity": 5e-2, "exposure": 1e1}
 
@@ -131,22 +134,32 @@ class LMProblem:
 
     # -------------------------------------------------------------- (J^T J + D) v
     def matvec(self, v, y):
-        """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view)."""
-        y.zero_()
-        self.local_normal_matvec(v, y)
-        self.damp_add(v, y)
-        return y
+        """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view; D v folded into the first view's gather)."""
+        return self.local_normal_matvec(v, y, damp=True)
 
-    def local_normal_matvec(self, v, y):
-        """y += sum over this problem's views of 2 J_b^T W_b J_b v (no damping)."""
+    def local_normal_matvec(self, v, y, damp=False):
+        """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y)."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
-        ys = self.layout.grads_struct(y, accumulate=True)
+        ys = self.layout.grads_struct(y)
+        if not self.views:
+            y.zero_()
+            if damp:
+                self.damp_add(v, y)
+            return y
         for b, vr in enumerate(self.views):
-            check(lib.gslm_matvec_view(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
-                                       self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
-                                       vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
-                                       vr.scratch.numel(), ctypes.byref(ys), self.stream), "gslm_matvec_view")
+            stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
+            check(lib.gslm_matvec_view_stages(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                              self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
+                                              vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
+                                              vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), stages,
+                                              self._damps if (damp and b == 0) else None, self.stream),
+                  "gslm_matvec_view_stages")
+        e0, e1 = self.layout.offsets["exposure"]
+        if damp:
+            torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
+        else:
+            y[e0:e1].zero_()
         return y
 
     def damp_add(self, v, y):

@@ -49,8 +49,9 @@ class ShardedLMProblem(LMProblem):
         return self._allreduce(out)
 
     def matvec(self, v, y):
-        y.zero_()
-        self.local_normal_matvec(v, y)
+        if self.world_size == 1:
+            return super().matvec(v, y)
+        self.local_normal_matvec(v, y, damp=False)
         self._allreduce(y)
         self.damp_add(v, y)
         return y

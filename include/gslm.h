@@ -153,10 +153,13 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
 #define GSLM_STAGE_RENDER 2
 #define GSLM_STAGE_GATHER 4
 #define GSLM_STAGE_ALL 7
+#define GSLM_STAGE_OVERWRITE 8 /* GATHER writes y instead of accumulating into it */
+/* damp7 (host array, GaussianModelDampMatrix order xyz, dc, rest, scaling, rotation, opacity,
+ * exposure) or NULL: when given, GATHER also adds D v (the exposure group is not touched). */
 int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                             const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                             int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
-                            const gslm_grads* y, int32_t stages, void* stream);
+                            const gslm_grads* y, int32_t stages, const double* damp7, void* stream);
 
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
