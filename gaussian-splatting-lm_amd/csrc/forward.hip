@@ -3,10 +3,10 @@
 //   k_preprocess   one thread per Gaussian: cull, project, cov3D, EWA cov2D, conic, radius,
 //                  rect, SH->RGB; writes a 48-B render record + depth key + tile count.
 //   (depth sort of P keys + scan of tile counts in depth order: sort.hip)
-//   k_duplicate    emits (tile id, dup index) pairs in depth order: the later *stable* sort on
+//   k_duplicate    emits (tile id, Gaussian id) pairs in depth order: the later *stable* sort on
 //                  the tile id alone then yields upstream's (tile, depth, index) order with
-//                  2 radix passes over N_dup instead of 6 (SURVEY §7 "Sort").
-//   k_finalize     point_list[k] = gid(dup[k]), inv[dup[k]] = k (slot of each dup entry).
+//                  2 radix passes over N_dup instead of 6 (SURVEY §7 "Sort"); the sorted values
+//                  ARE the point list.
 //   k_ranges       per-tile [start, end) from key changes (identifyTileRanges).
 //   k_render_fwd   one 16x16 tile per 256-thread block (4 wave64), Gaussian records staged
 //                  through LDS 256 at a time, __syncthreads_count early exit (renderCUDA).
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
       if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, b.y * expf(power));
+      const float alpha = fminf(0.99f, b.y * gexp(power));
       if (alpha < 1.0f / 255.0f) continue;
       const float test_T = T * (1.0f - alpha);
       if (test_T < 0.0001f) {

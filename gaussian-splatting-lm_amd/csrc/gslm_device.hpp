@@ -193,6 +193,20 @@ __device__ __forceinline__ float ndc2pix(float v, int S) {
   return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
 }
 
+// exp of the Gaussian falloff in the tile passes.  Every GPU tile pass (forward, JVP, VJP, fused
+// matvec) uses this same function, so their skip / stop decisions agree bit for bit with each
+// other.  Default: the hardware exp2 path (v_exp_f32, ~2 ulp); -DGSLM_PRECISE_EXP selects the
+// correctly-rounded-ish libm expf (closer to the CPU oracle's decisions, ~10 more instructions).
+__device__ __forceinline__ float gexp(float x) {
+#ifdef GSLM_PRECISE_EXP
+  return expf(x);
+#else
+  return __expf(x);
+#endif
+}
+// 1/x via v_rcp_f32 (1 ulp); used where upstream divides T by (1 - alpha)
+__device__ __forceinline__ float rcp_f(float x) { return __builtin_amdgcn_rcpf(x); }
+
 // numerically stable sigmoid matching torch.sigmoid for float
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 

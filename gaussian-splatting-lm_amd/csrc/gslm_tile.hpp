@@ -28,6 +28,38 @@ __device__ __forceinline__ float wave_sum_lane63(float x) {
   return x;
 }
 
+// Transposed ("reduce-scatter") sum of 8 values per lane over the 64 lanes of a wave, using the
+// gfx950 permlane swaps for the cross-half steps and DPP inside rows.  On return every lane of the
+// 8-lane group k (lanes 8k..8k+7) holds sum over the wave of v[k].  18 instructions instead of
+// 8 x 6 DPP adds.  Requires all 64 lanes active.
+__device__ __forceinline__ float perm32_add(float a, float b, float& hi_part) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  (void)hi_part;
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float perm16_add(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float wave_reduce8_t(const float v[8], int lane) {
+  float dummy = 0.f;
+  // step 1 (lanes l <-> l+32): lower half keeps values 0..3, upper half values 4..7
+  const float w0 = perm32_add(v[0], v[4], dummy), w1 = perm32_add(v[1], v[5], dummy);
+  const float w2 = perm32_add(v[2], v[6], dummy), w3 = perm32_add(v[3], v[7], dummy);
+  // step 2 (rows r <-> r^1): even rows keep w0, w1; odd rows keep w2, w3
+  const float u0 = perm16_add(w0, w2), u1 = perm16_add(w1, w3);
+  // step 3 (lanes l <-> l^8 inside a row): bit3 = 0 keeps u0, bit3 = 1 keeps u1
+  const bool hi8 = (lane & 8) != 0;
+  const float give = hi8 ? u0 : u1;
+  float x = hi8 ? u1 : u0;
+  x += dpp_f<0x128>(give);  // row_ror:8
+  // step 4: sum the 8 lanes of the group
+  x += dpp_f<0xB1>(x);      // quad_perm [1,0,3,2]
+  x += dpp_f<0x4E>(x);      // quad_perm [2,3,0,1]
+  x += dpp_f<0x141>(x);     // row_half_mirror
+  return x;                 // value index of this lane: (lane >> 3) & 7
+}
+
 // Screen-space gradient of one (tile, Gaussian) pair, value index q:
 //   0 dL/dx_pix  1 dL/dy_pix  2 dL/dconic.a  3 dL/dconic.b  4 dL/dconic.c  5 dL/dopacity_eff
 //   6..8 dL/drgb  9 dL/dinvdepth
@@ -151,14 +183,15 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       const float4 c = s_r2[j];
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      const float G = expf(power);
+      const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
       const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
       float gv[NV];
 #pragma unroll
       for (int q = 0; q < NV; ++q) gv[q] = 0.f;
       if (valid) {
-        st.T = st.T / (1.f - alpha);
+        const float inv1ma = rcp_f(1.f - alpha);
+        st.T = st.T * inv1ma;
         const float dchannel = alpha * st.T;
         const float col[3] = {b.z, b.w, c.x};
         float dL_dalpha = 0.f;
@@ -178,7 +211,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         }
         dL_dalpha *= st.T;
         st.last_alpha = alpha;
-        dL_dalpha += (-st.T_final / (1.f - alpha)) * st.bg_dot;
+        dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
         const float dL_dG = b.y * dL_dalpha;
         const float gdx = G * dx, gdy = G * dy;
         if (WITH_XY) {
@@ -191,16 +224,32 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         gv[5] = G * dL_dalpha;
       }
       const bool any = __ballot(valid) != 0ull;
-      if (any) {
+      if constexpr (NU <= 8) {
+        // transposed reduction: value slot k ends in lanes 8k..8k+7; lane 8k stores it
+        float r = 0.f;
+        if (any) {
+          float pv[8];
 #pragma unroll
-        for (int q = 0; q < NV; ++q)
-          if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
-      }
-      if (lane == 63) {
+          for (int k = 0; k < 8; ++k) pv[k] = 0.f;
 #pragma unroll
-        for (int q = 0; q < NV; ++q)
-          if (q_used<WITH_XY, WITH_INV>(q))
-            s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
+          for (int q = 0; q < NV; ++q)
+            if (q_used<WITH_XY, WITH_INV>(q)) pv[q_slot<WITH_XY, WITH_INV>(q)] = gv[q];
+          r = wave_reduce8_t(pv, lane);
+        }
+        const int k = lane >> 3;
+        if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * TILE_PIX + j] = r;
+      } else {
+        if (any) {
+#pragma unroll
+          for (int q = 0; q < NV; ++q)
+            if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
+        }
+        if (lane == 63) {
+#pragma unroll
+          for (int q = 0; q < NV; ++q)
+            if (q_used<WITH_XY, WITH_INV>(q))
+              s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
+        }
       }
     }
     __syncthreads();

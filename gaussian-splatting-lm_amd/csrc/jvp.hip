@@ -68,7 +68,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
       const float4 b = s_r1[j];
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      const float G = expf(power);
+      const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
       if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
         const float4 c = s_r2[j];

@@ -100,6 +100,7 @@ EXPORTS = {
                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p]),
+    "gslm_selftest": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_last_error": (ctypes.c_char_p, []),
     "gslm_abi_version": (ctypes.c_int, []),
 }

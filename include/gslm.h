@@ -184,6 +184,11 @@ int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t num_r
                  const void* image, uint32_t* point_list, uint32_t* ranges, uint32_t* tiles_touched,
                  float* final_T, uint32_t* n_contrib, float* records, void* stream);
 
+/* Device self-test of the wave primitives (one 64-lane wave).  in: [64][8] floats, out: [64].
+ * which = 0: transposed 8-value reduction (lane l returns the sum of value (l >> 3) & 7);
+ * which = 1: DPP sum of in[l*8] (lane 63 returns the total). */
+int gslm_selftest(int32_t which, const float* in, float* out, void* stream);
+
 const char* gslm_last_error(void);
 int gslm_abi_version(void);
 
