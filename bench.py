@@ -142,10 +142,13 @@ def main():
     lib, check = _lib.lib, _lib.check
 
     def stage(mask):
-        check(lib.gslm_matvec_view_stages(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
-                                          prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
-                                          vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
-                                          ctypes.byref(ys), mask, None, prob.stream))
+        opts = _lib.GslmMatvecOpts()
+        opts.stages = mask | (8 if mask == 4 else 0)  # the gather in its CG form: overwrite + D v
+        opts.damp7 = prob._damps if mask == 4 else None
+        check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
+                                      prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                      vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                      ctypes.byref(ys), ctypes.byref(opts), prob.stream))
 
     stage(1)
     stage(2)

@@ -318,14 +318,21 @@ int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussia
                     (hipStream_t)stream);
 }
 
-int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
-                            const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
-                            int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
-                            int32_t stages, const double* damp7, void* stream) {
+int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
+                        const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
+                        int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
+                        const gslm_matvec_opts* opts, void* stream) {
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;
   if (!vin || !y || !pixel_weight) { set_error("matvec: NULL argument"); return GSLM_ERR_INVALID; }
+  const int32_t stages = (opts && opts->stages) ? opts->stages : GSLM_STAGE_ALL;
+  const double* damp7 = opts ? opts->damp7 : nullptr;
+  double* dot_out = opts ? opts->dot_vy : nullptr;
+  if (dot_out && (!opts->dot_scratch || opts->dot_scratch_bytes < gslm_dot_scratch_bytes(b.g.P))) {
+    set_error("matvec: dot scratch too small");
+    return GSLM_ERR_CAPACITY;
+  }
   if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
@@ -334,15 +341,19 @@ int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* gi, con
       (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
     return st;
   if (!(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
-  return launch_gather_lm(b.v, b.g, b.gb, b.sb, make_gradk(y), make_gradk(vin), damp7,
-                          (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, s);
+  double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
+  if ((st = launch_gather_lm(b.v, b.g, b.gb, b.sb, make_gradk(y), make_gradk(vin), damp7,
+                             (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, part, s)))
+    return st;
+  if (dot_out) return gslm_dot_finalize(part, (int32_t)((b.g.P + 255) / 256), dot_out, stream);
+  return GSLM_OK;
 }
 
 int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
                      const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning, int64_t N,
                      const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y, void* stream) {
-  return gslm_matvec_view_stages(view, gi, vin, pixel_weight, mask_xyz, geom, binning, N, image, scratch,
-                                 scratch_bytes, y, GSLM_STAGE_ALL, nullptr, stream);
+  return gslm_matvec_view_ex(view, gi, vin, pixel_weight, mask_xyz, geom, binning, N, image, scratch, scratch_bytes,
+                             y, nullptr, stream);
 }
 
 int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, int32_t H, int32_t W,

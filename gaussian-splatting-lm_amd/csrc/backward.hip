@@ -87,13 +87,21 @@ struct FlatK {
   float damp[6];
   int use_damp;
   int overwrite;
+  double* dot_part;   // per-block partials of <v, y> over the written elements (NULL = off)
 };
 
-__device__ __forceinline__ void emit(float* y, const float* v, float d, int use_damp, int overwrite, int64_t idx,
-                                     float val) {
-  if (use_damp) val += d * v[idx];
+// y[idx] (op)= val (+ d v[idx]); returns v[idx] * y_new for the fused <v, y> (0 when dot is off)
+__device__ __forceinline__ double emit(float* y, const float* v, float d, int use_damp, int overwrite, bool dot,
+                                       int64_t idx, float val) {
+  const float vv = (use_damp || dot) ? v[idx] : 0.f;
+  if (use_damp) val += d * vv;
+  float out = val;
   if (overwrite) y[idx] = val;
-  else y[idx] += val;
+  else {
+    out = y[idx] + val;
+    y[idx] = out;
+  }
+  return dot ? (double)vv * (double)out : 0.0;
 }
 
 template <bool WANT_MEANS, int ROWF4>
@@ -102,11 +110,14 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
                                                     const uint32_t* __restrict__ goff,
                                                     const float4* __restrict__ rows, FlatK o) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(K-1)]
+  __shared__ double s_dot[4];
   const int tid = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + tid;
   const int R = 3 * (g.M - 1);
   const int nc = (v.D + 1) * (v.D + 1);
+  const bool dot = o.dot_part != nullptr;
+  double dacc = 0.0;
   if (i < g.P) {
     const uint32_t n = tiles[i];
     float G2[NV];
@@ -116,18 +127,18 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
     const int u = o.use_damp, ow = o.overwrite;
     if (WANT_MEANS) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) emit(o.y[0], o.v[0], o.damp[0], u, ow, 3 * i + k, co.dmean[k]);
+      for (int k = 0; k < 3; ++k) dacc += emit(o.y[0], o.v[0], o.damp[0], u, ow, dot, 3 * i + k, co.dmean[k]);
     } else if (ow) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) o.y[0][3 * i + k] = u ? o.damp[0] * o.v[0][3 * i + k] : 0.f;
+      for (int k = 0; k < 3; ++k) dacc += emit(o.y[0], o.v[0], o.damp[0], u, 1, dot && u, 3 * i + k, 0.f);
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) emit(o.y[1], o.v[1], o.damp[1], u, ow, 3 * i + k, co.dsh[0][k]);
+    for (int k = 0; k < 3; ++k) dacc += emit(o.y[1], o.v[1], o.damp[1], u, ow, dot, 3 * i + k, co.dsh[0][k]);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) emit(o.y[3], o.v[3], o.damp[3], u, ow, 3 * i + k, co.dscale[k]);
+    for (int k = 0; k < 3; ++k) dacc += emit(o.y[3], o.v[3], o.damp[3], u, ow, dot, 3 * i + k, co.dscale[k]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) emit(o.y[4], o.v[4], o.damp[4], u, ow, 4 * i + k, co.drot[k]);
-    emit(o.y[5], o.v[5], o.damp[5], u, ow, i, co.dop);
+    for (int k = 0; k < 4; ++k) dacc += emit(o.y[4], o.v[4], o.damp[4], u, ow, dot, 4 * i + k, co.drot[k]);
+    dacc += emit(o.y[5], o.v[5], o.damp[5], u, ow, dot, i, co.dop);
 #pragma unroll
     for (int k = 1; k < 16; ++k)
       if (k < g.M) {
@@ -140,7 +151,15 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
   const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
   const int64_t base = i0 * R;
   for (int64_t e = tid; e < nvalid * R; e += blockDim.x)
-    emit(o.y[2], o.v[2], o.damp[2], o.use_damp, o.overwrite, base + e, s_rest[e]);
+    dacc += emit(o.y[2], o.v[2], o.damp[2], o.use_damp, o.overwrite, dot, base + e, s_rest[e]);
+  if (dot) {
+    const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dacc += __shfl_down(dacc, off, 64);
+    if (lane == 0) s_dot[w] = dacc;
+    __syncthreads();
+    if (tid == 0) o.dot_part[blockIdx.x] = ((s_dot[0] + s_dot[1]) + s_dot[2]) + s_dot[3];
+  }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -174,7 +193,8 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
 }
 
 int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
-                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, hipStream_t s) {
+                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
+                     hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   if (g.cov3D || g.colors || !g.raw || y.rest_stride != 3 * (g.M - 1) || y.dc_stride != 3) {
     set_error("LM gather expects raw leaves with SH colours and a flat param-space output");
@@ -187,7 +207,8 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
   for (int k = 0; k < 6; ++k) o.damp[k] = damp7 ? (float)damp7[k] : 0.f;
   o.use_damp = damp7 ? 1 : 0;
   o.overwrite = overwrite ? 1 : 0;
-  if (o.use_damp)
+  o.dot_part = dot_part;
+  if (o.use_damp || dot_part)
     for (int k = 0; k < 6; ++k)
       if (!o.v[k] && !(k == 2 && g.M == 1)) { set_error("damping needs every group of v"); return GSLM_ERR_INVALID; }
   const unsigned nb = (unsigned)((g.P + 255) / 256);

@@ -89,6 +89,41 @@ __global__ __launch_bounds__(256) void k_xpby_dev(int64_t n, const float* __rest
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = s[i] + b * p[i];
 }
 
+// One CG step on flat vectors, a = gam / del (device scalars):
+//   x += a p ;  s -= a q ;  part[block] = sum s_new^2     (then k_dot_final -> gamma')
+__global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const double* __restrict__ gam,
+                                                           const double* __restrict__ del,
+                                                           const float* __restrict__ p, const float* __restrict__ q,
+                                                           float* __restrict__ x, float* __restrict__ s,
+                                                           double* __restrict__ part) {
+  __shared__ double sm[DOT_THREADS / 64];
+  const float a = (float)((*gam) / (*del));
+  double acc = 0.0;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * DOT_THREADS;
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+  const float4* q4 = reinterpret_cast<const float4*>(q);
+  float4* x4 = reinterpret_cast<float4*>(x);
+  float4* s4 = reinterpret_cast<float4*>(s);
+  for (int64_t i = (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n4; i += stride) {
+    const float4 pv = p4[i], qv = q4[i];
+    float4 xv = x4[i], sv = s4[i];
+    xv.x += a * pv.x; xv.y += a * pv.y; xv.z += a * pv.z; xv.w += a * pv.w;
+    sv.x -= a * qv.x; sv.y -= a * qv.y; sv.z -= a * qv.z; sv.w -= a * qv.w;
+    x4[i] = xv;
+    s4[i] = sv;
+    acc += (double)sv.x * sv.x + (double)sv.y * sv.y + (double)sv.z * sv.z + (double)sv.w * sv.w;
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n; i += stride) {
+    x[i] += a * p[i];
+    const float sv = s[i] - a * q[i];
+    s[i] = sv;
+    acc += (double)sv * sv;
+  }
+  const double t = block_sum_d(acc, sm);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
 __global__ __launch_bounds__(256) void k_damp_add(int64_t n, const float* __restrict__ x, Groups g,
                                                   float* __restrict__ y) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -121,8 +156,30 @@ using namespace gslm;
 extern "C" {
 
 size_t gslm_dot_scratch_bytes(int64_t n) {
-  (void)n;
-  return DOT_BLOCKS * sizeof(double);
+  const int64_t per_block = (n + 255) / 256 + 16;  // partials of a per-Gaussian fused dot
+  return (size_t)(per_block > DOT_BLOCKS ? per_block : DOT_BLOCKS) * sizeof(double);
+}
+
+int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q, float* x,
+                   float* s, void* scratch, double* gam_new_dev, void* stream) {
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(x) |
+       reinterpret_cast<uintptr_t>(s)) & 15) {
+    set_error("gslm_cg_update: vectors must be 16-byte aligned");
+    return GSLM_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_cg_update, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s,
+                     (double*)scratch);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, (const double*)scratch, DOT_BLOCKS, gam_new_dev);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* stream) {
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, (hipStream_t)stream, (const double*)partials, np,
+                     out_dev);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
 }
 
 int gslm_dot(const float* a, const float* b, const int64_t* group_bounds, const double* group_damp, int32_t ngroups,

@@ -209,5 +209,6 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
                          const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s);
 int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
-                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, hipStream_t s);
+                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
+                     hipStream_t s);
 }  // namespace gslm

@@ -50,6 +50,14 @@ class GslmGrads(ctypes.Structure):
     ]
 
 
+class GslmMatvecOpts(ctypes.Structure):
+    _fields_ = [
+        ("stages", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("damp7", ctypes.POINTER(ctypes.c_double)), ("dot_vy", ctypes.c_void_p),
+        ("dot_scratch", ctypes.c_void_p), ("dot_scratch_bytes", ctypes.c_size_t),
+    ]
+
+
 # Every symbol include/gslm.h declares; tests check the library exports each of them.
 EXPORTS = {
     "gslm_geom_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
@@ -80,11 +88,15 @@ EXPORTS = {
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
                                         ctypes.c_void_p]),
-    "gslm_matvec_view_stages": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
-                                               ctypes.POINTER(GslmGrads), ctypes.c_void_p, ctypes.c_int32,
-                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
-                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p]),
+    "gslm_matvec_view_ex": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
+                                           ctypes.POINTER(GslmGrads), ctypes.c_void_p, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_cg_update": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_dot_finalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_dot_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gslm_dot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                 ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,

@@ -86,7 +86,8 @@ class LMProblem:
         self.masks = [c.alpha_mask.to(device) for c in cams] if alpha_masks is None else alpha_masks
         self.views = [ViewRaster(_lib.view_from_camera(c, bg, model.active_sh_degree), device) for c in cams]
         self.stream = _lib.stream_handle(device)
-        self.dot_scratch = torch.empty(lib.gslm_dot_scratch_bytes(0) // 8 + 8, dtype=torch.float64, device=device)
+        self.dot_scratch = torch.empty(lib.gslm_dot_scratch_bytes(max(P, self.layout.numel)) // 8 + 8,
+                                       dtype=torch.float64, device=device)
         self.weights = [None] * len(cams)
         self.residuals = [None] * len(cams)
 
@@ -135,9 +136,17 @@ class LMProblem:
     # -------------------------------------------------------------- (J^T J + D) v
     def matvec(self, v, y):
         """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view; D v folded into the first view's gather)."""
-        return self.local_normal_matvec(v, y, damp=True)
+        self.matvec_dot(v, y, None)
+        return y
 
-    def local_normal_matvec(self, v, y, damp=False):
+    def matvec_dot(self, v, y, dot_out):
+        """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
+        view; exposure components of v zero, as in every LM iterate).  Returns True if fused."""
+        fuse = dot_out is not None and len(self.views) == 1
+        self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None)
+        return fuse
+
+    def local_normal_matvec(self, v, y, damp=False, dot_out=None):
         """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y)."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
@@ -147,14 +156,20 @@ class LMProblem:
             if damp:
                 self.damp_add(v, y)
             return y
+        last = len(self.views) - 1
         for b, vr in enumerate(self.views):
-            stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
-            check(lib.gslm_matvec_view_stages(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
-                                              self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
-                                              vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
-                                              vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), stages,
-                                              self._damps if (damp and b == 0) else None, self.stream),
-                  "gslm_matvec_view_stages")
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
+            opts.damp7 = self._damps if (damp and b == 0) else None
+            if dot_out is not None and b == last:
+                opts.dot_vy = dot_out
+                opts.dot_scratch = self.dot_scratch.data_ptr()
+                opts.dot_scratch_bytes = self.dot_scratch.numel() * 8
+            check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                          self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
+                                          vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
+                                          vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts), self.stream),
+                  "gslm_matvec_view_ex")
         e0, e1 = self.layout.offsets["exposure"]
         if damp:
             torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
@@ -190,11 +205,11 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     st = prob.stream
     sc = torch.zeros(16, dtype=torch.float64, device=dev)
     ptr = lambda i: sc.data_ptr() + 8 * i
-    GAM, DEL, GAMN, XG, XS = 0, 1, 2, 3, 4
+    GAM, GAMN, DEL, XG, XS = 0, 1, 2, 3, 4  # gamma / gamma' ping-pong between slots 0 and 1
     x = torch.zeros(n, dtype=torch.float32, device=dev)
     s = torch.empty_like(x)
     p = torch.empty_like(x)
-    q = torch.empty_like(x)
+    q = torch.zeros_like(x)
     b2 = float(prob.loss) if check_every else None  # ||b||^2 = loss
     iter_total, last_res, history = 0, math.inf, []
     first = True
@@ -209,16 +224,17 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
         prob.dot(s, s, ptr(GAM))
         stop = False
         for _ in range(restart_iter):
-            prob.matvec(p, q)
-            prob.dot(p, q, ptr(DEL))
+            # q = A p and delta = <p, A p> (= |J p|^2 + p.D.p), fused into the gather when possible
+            if not prob.matvec_dot(p, q, ptr(DEL)):
+                prob.dot(p, q, ptr(DEL))
             if check_every and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
                 stop = True
                 break
-            check(lib.gslm_axpy_dev(n, ptr(GAM), ptr(DEL), 1.0, p.data_ptr(), x.data_ptr(), st))
-            check(lib.gslm_axpy_dev(n, ptr(GAM), ptr(DEL), -1.0, q.data_ptr(), s.data_ptr(), st))
-            prob.dot(s, s, ptr(GAMN))
+            # x += alpha p ; s -= alpha q ; gamma' = <s, s>   (one pass)
+            check(lib.gslm_cg_update(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(), s.data_ptr(),
+                                     prob.dot_scratch.data_ptr(), ptr(GAMN), st))
             check(lib.gslm_xpby_dev(n, s.data_ptr(), ptr(GAMN), ptr(GAM), p.data_ptr(), st))
             if check_every:
                 prob.dot(x, g, ptr(XG))
@@ -237,7 +253,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                     break
             if callback is not None:
                 callback(x, s, iter_total + 1)
-            sc[GAM].copy_(sc[GAMN])
+            GAM, GAMN = GAMN, GAM
             iter_total += 1
             if iter_total >= max_iter:
                 stop = True

@@ -48,10 +48,10 @@ class ShardedLMProblem(LMProblem):
         super().rhs(out)
         return self._allreduce(out)
 
-    def matvec(self, v, y):
+    def matvec_dot(self, v, y, dot_out):
         if self.world_size == 1:
-            return super().matvec(v, y)
+            return super().matvec_dot(v, y, dot_out)
         self.local_normal_matvec(v, y, damp=False)
         self._allreduce(y)
         self.damp_add(v, y)
-        return y
+        return False

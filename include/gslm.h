@@ -154,12 +154,19 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
 #define GSLM_STAGE_GATHER 4
 #define GSLM_STAGE_ALL 7
 #define GSLM_STAGE_OVERWRITE 8 /* GATHER writes y instead of accumulating into it */
-/* damp7 (host array, GaussianModelDampMatrix order xyz, dc, rest, scaling, rotation, opacity,
- * exposure) or NULL: when given, GATHER also adds D v (the exposure group is not touched). */
-int gslm_matvec_view_stages(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
-                            const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
-                            int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
-                            const gslm_grads* y, int32_t stages, const double* damp7, void* stream);
+typedef struct gslm_matvec_opts {
+  int32_t stages;         /* GSLM_STAGE_* bits; 0 means GSLM_STAGE_ALL (accumulate) */
+  int32_t reserved;
+  const double* damp7;    /* host array (GaussianModelDampMatrix order: xyz, dc, rest, scaling, rotation,
+                             opacity, exposure) or NULL; when set GATHER also adds D v (exposure untouched) */
+  double* dot_vy;         /* device double or NULL: receives <v, y> over the gathered groups after GATHER */
+  void* dot_scratch;      /* device scratch for dot_vy, >= gslm_dot_scratch_bytes(P) bytes */
+  size_t dot_scratch_bytes;
+} gslm_matvec_opts;
+int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
+                        const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
+                        int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
+                        const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
 
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
@@ -173,6 +180,12 @@ int gslm_axpy_dev(int64_t n, const double* num_dev, const double* den_dev, float
 /* p = s + beta p, beta = num/den from device memory */
 int gslm_xpby_dev(int64_t n, const float* s, const double* num_dev, const double* den_dev, float* p,
                   void* stream);
+/* One CG step, a = gam / del read from device memory:  x += a p;  s -= a q;
+ * *gam_new_dev = <s, s> (scratch >= gslm_dot_scratch_bytes(n)).  Vectors 16-byte aligned. */
+int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
+                   float* x, float* s, void* scratch, double* gam_new_dev, void* stream);
+/* *out_dev = sum of np per-block partials (second pass of the fused dots) */
+int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* stream);
 /* y += d[group] * x (the damping term D x) */
 int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const double* group_damp,
                   int32_t ngroups, float* y, void* stream);

@@ -90,6 +90,32 @@ def test_matvec_deterministic():
     assert torch.equal(y1, y2)
 
 
+def test_fused_dot_and_cg_update():
+    """<v, A v> fused into the gather and the one-pass CG update match plain torch algebra."""
+    from gslm import _lib
+    from gslm.lm import LMProblem
+    d, m, cams = _load()
+    prob = LMProblem(m, cams[:1], torch.zeros(3))
+    prob.evaluate()
+    v = torch.from_numpy(d["v"]).cuda()
+    sc = torch.zeros(4, dtype=torch.float64, device="cuda")
+    y = prob.zeros()
+    assert prob.matvec_dot(v, y, sc.data_ptr())
+    ref = (v.double() * y.double()).sum()
+    assert abs(sc[0].item() - ref.item()) <= 1e-9 * abs(ref.item())
+    # x += a p ; s -= a q ; gamma' = <s, s>
+    g = torch.Generator().manual_seed(5)
+    p, q, x, s = (torch.randn(v.numel(), generator=g).cuda() for _ in range(4))
+    x0, s0 = x.clone(), s.clone()
+    sc[1], sc[2] = 3.0, 2.0
+    _lib.check(_lib.lib.gslm_cg_update(v.numel(), sc.data_ptr() + 8, sc.data_ptr() + 16, p.data_ptr(), q.data_ptr(),
+                                       x.data_ptr(), s.data_ptr(), prob.dot_scratch.data_ptr(), sc.data_ptr() + 24,
+                                       _lib.stream_handle()))
+    torch.cuda.synchronize()
+    assert torch.allclose(x, x0 + 1.5 * p, atol=1e-6) and torch.allclose(s, s0 - 1.5 * q, atol=1e-6)
+    assert abs(sc[3].item() - (s.double() ** 2).sum().item()) <= 1e-9 * sc[3].item()
+
+
 def test_lm_step_decreases_loss():
     from gslm.lm import lm_step
     d, m, cams = _load()
