@@ -2,18 +2,18 @@
 
 The reference has no distributed code: its LinearSolverFunctions renders a view batch
 serially on one GPU (solver_functions.py:38-41,88-93,110-121).  Here every rank owns a disjoint
-slice of the camera batch; the parameters theta (59 fp32 per Gaussian at SH 3) are replicated.
+block of the camera batch; the parameters theta (59 fp32 per Gaussian at SH 3) are replicated.
   * J v and the per-view weights never leave the GPU that renders the view;
   * the only exchange per CG iteration is ONE all-reduce (sum) of the partial J^T W J v over the
     param-space vector (SURVEY §8(e)); D v is added after the reduction, once;
   * J^T b and the loss are all-reduced once per LM step.
 All-reduce results are bitwise identical on every rank, so the CG scalars (computed redundantly on
 each rank, device-resident) stay consistent without a further broadcast.
-"""
-import torch
-import torch.distributed as dist
 
-from gslm.lm import LMProblem
+`ShardedOperator` wraps any per-rank operator with the LMProblem protocol (gslm.lm.LMProblem on
+the GPU, oracle.lm_ref.OracleLMProblem in the CPU tests).
+"""
+import torch.distributed as dist
 
 
 def world():
@@ -29,11 +29,14 @@ def shard_views(n_views, rank, world_size):
     return list(range(lo, min(lo + per, n_views)))
 
 
-class ShardedLMProblem(LMProblem):
-    def __init__(self, model, cams, bg, group=None, **kw):
-        super().__init__(model, cams, bg, **kw)
+class ShardedOperator:
+    def __init__(self, local, group=None):
+        self.local = local
         self.group = group
         self.rank, self.world_size = world()
+
+    def __getattr__(self, name):  # layout, dot, zeros, stream, dot_scratch, views, ...
+        return getattr(self.local, name)
 
     def _allreduce(self, t):
         if self.world_size > 1:
@@ -41,17 +44,33 @@ class ShardedLMProblem(LMProblem):
         return t
 
     def evaluate(self):
-        loss = super().evaluate()
-        return self._allreduce(loss)
+        loss = self.local.evaluate()
+        self._allreduce(loss)
+        self.local.loss = loss
+        return loss
+
+    @property
+    def loss(self):
+        return self.local.loss
 
     def rhs(self, out):
-        super().rhs(out)
+        self.local.rhs(out)
         return self._allreduce(out)
 
     def matvec_dot(self, v, y, dot_out):
         if self.world_size == 1:
-            return super().matvec_dot(v, y, dot_out)
-        self.local_normal_matvec(v, y, damp=False)
+            return self.local.matvec_dot(v, y, dot_out)
+        self.local.local_normal_matvec(v, y, damp=False)
         self._allreduce(y)
-        self.damp_add(v, y)
+        self.local.damp_add(v, y)
         return False
+
+    def matvec(self, v, y):
+        self.matvec_dot(v, y, None)
+        return y
+
+
+def ShardedLMProblem(model, cams, bg, group=None, **kw):
+    """LMProblem over this rank's views, wrapped for the cross-rank reductions."""
+    from gslm.lm import LMProblem
+    return ShardedOperator(LMProblem(model, cams, bg, **kw), group=group)

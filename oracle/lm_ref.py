@@ -1,0 +1,162 @@
+"""ORACLE -- test infrastructure only: the LM normal equations on the CPU oracle renderer.
+
+A PyTorch restatement of the reference LM algebra around
+oracle/torch_raster.py, used to (1) check the oracle-side solver semantics against the golden
+vectors the reference's own solver produced (tests/golden/solver_golden.npz) and (2) stand in for
+the HIP operator in multi-process (gloo) tests of the view sharding:
+
+  residual        r_b = m_b * clamp01(R_b) - gt_b, residual vector [r; r]
+                  (batch_training_loss.py:10-17, disable_ssim=True)
+  J^T b           -2 sum_b J_r^T r_b                      (solver_functions.py:101-132 with b = -[r; r])
+  (J^T J + D) v   2 sum_b J_r^T J_r v + D v               (matvec, matvec_T, GaussianModelDampMatrix)
+  CGLS            conjugate_gradient.py:51-127 in its normal-equations form, float64 scalars
+"""
+import math
+
+import torch
+import torch.autograd.forward_ad as fwAD
+
+from gslm.params import GROUPS, ParamLayout
+from oracle import torch_raster as tr
+
+DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
+                "opacity": 5e-2, "exposure": 1e1}
+
+
+class OracleLMProblem:
+    def __init__(self, model, cams, bg, mask_xyz=True, damp=None):
+        self.model, self.cams, self.bg = model, cams, bg
+        self.mask_xyz = mask_xyz
+        self.damp = DEFAULT_DAMP if damp is None else damp
+        P = model._xyz.shape[0]
+        K = 1 + model._features_rest.shape[1]
+        self.layout = ParamLayout(P, K, model._exposure.shape[0])
+
+    def _leaves(self):
+        m = self.model
+        return [m._xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure]
+
+    def _residuals(self):
+        out = []
+        for c in self.cams:
+            img, _, _, _ = tr.render_model(self.model, c, self.bg)
+            out.append(img * c.alpha_mask - c.original_image)
+        return out
+
+    def evaluate(self):
+        with torch.no_grad():
+            self.loss = sum(2.0 * (r.double() ** 2).sum() for r in self._residuals())
+        return self.loss
+
+    def _flatten(self, tensors):
+        return torch.cat([t.reshape(-1) for t in tensors])
+
+    def _mask(self, vec):
+        o = self.layout.offsets
+        if self.mask_xyz:
+            vec[o["xyz"][0]:o["xyz"][1]] = 0
+        vec[o["exposure"][0]:o["exposure"][1]] = 0
+        return vec
+
+    def rhs(self, out=None):
+        leaves = self._leaves()
+        for t in leaves:
+            t.grad = None
+        loss = sum((r * r).sum() for r in self._residuals())
+        grads = torch.autograd.grad(loss, leaves, allow_unused=True)
+        g = self._flatten([-(gr if gr is not None else torch.zeros_like(t)) for gr, t in zip(grads, leaves)])
+        g = self._mask(g.detach())
+        if out is not None:
+            out.copy_(g)
+            return out
+        return g
+
+    def _jr_v(self, v):
+        views = self.layout.views(v)
+        m = self.model
+        saved = self._leaves()
+        with torch.no_grad(), fwAD.dual_level():
+            (m._xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure) = [
+                fwAD.make_dual(t.detach(), views[gname].to(t.dtype)) for t, gname in zip(saved, GROUPS)]
+            try:
+                tangents = [fwAD.unpack_dual(r).tangent for r in self._residuals()]
+            finally:
+                (m._xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure) = saved
+        return [t if t is not None else torch.zeros(3, c.image_height, c.image_width)
+                for t, c in zip(tangents, self.cams)]
+
+    def damp_add(self, v, y):
+        for gname in GROUPS:
+            a, b = self.layout.offsets[gname]
+            y[a:b] += self.damp[gname] * v[a:b]
+        return y
+
+    def local_normal_matvec(self, v, y, damp=False):
+        """y = [D v +] sum_b 2 J_r^T J_r v (overwrites y)."""
+        v = self._mask(v.clone())
+        jv = self._jr_v(v)
+        leaves = self._leaves()
+        res = self._residuals()
+        obj = sum((r * (2.0 * t.detach())).sum() for r, t in zip(res, jv))
+        grads = torch.autograd.grad(obj, leaves, allow_unused=True)
+        out = self._flatten([gr if gr is not None else torch.zeros_like(t) for gr, t in zip(grads, leaves)])
+        y.copy_(self._mask(out.detach()))
+        if damp:
+            self.damp_add(v, y)
+        return y
+
+    def matvec(self, v, y):
+        return self.local_normal_matvec(v, y, damp=True)
+
+    def matvec_dot(self, v, y, dot_out):
+        self.matvec(v, y)
+        return False
+
+    def zeros(self):
+        return torch.zeros(self.layout.numel)
+
+
+def cgls_ref(op, g, max_iter, restart_iter, tol=1e-10, atol=0.0):
+    """cgls_damped (conjugate_gradient.py:51-127) written on A = J^T J + D in float64 scalars.
+    Same restart schedule and stopping tests as gslm.lm.cgls_fused."""
+    n = g.numel()
+    x = torch.zeros(n, dtype=g.dtype)
+    b2 = float(op.loss)
+    iter_total, last_res, first = 0, math.inf, True
+    q = torch.zeros_like(x)
+    while iter_total < max_iter:
+        if first:
+            s = g.clone()
+            first = False
+        else:
+            s = g - op.matvec(x, q)
+        p = s.clone()
+        gamma = float((s.double() * s.double()).sum())
+        stop = False
+        for _ in range(restart_iter):
+            op.matvec(p, q)
+            delta = float((p.double() * q.double()).sum())
+            if delta < 1e-20:
+                stop = True
+                break
+            alpha = gamma / delta
+            x = x + alpha * p
+            s = s - alpha * q
+            gamma_new = float((s.double() * s.double()).sum())
+            p = s + (gamma_new / gamma) * p
+            res = b2 - float((x.double() * g.double()).sum()) - float((x.double() * s.double()).sum())
+            if res > last_res:
+                stop = True
+                break
+            last_res = res
+            if gamma_new < max(tol * math.sqrt(gamma), atol):
+                stop = True
+                break
+            gamma = gamma_new
+            iter_total += 1
+            if iter_total >= max_iter:
+                stop = True
+                break
+        if stop:
+            break
+    return x
