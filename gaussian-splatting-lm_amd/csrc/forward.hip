@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
 
   const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
   const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
-  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.depth);
+  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), __uint_as_float(o.ext));
   rec[3 * i + 0] = r0;
   rec[3 * i + 1] = r1;
   rec[3 * i + 2] = r2;
@@ -76,10 +76,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
                                                      const float4* __restrict__ rec, float* __restrict__ out_color,
                                                      float* __restrict__ out_invdepth, float* __restrict__ final_T,
                                                      uint32_t* __restrict__ n_contrib) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_r2[TILE_PIX];
+  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
+  __shared__ float2 s_r2[TILE_PIX];
+  __shared__ uint64_t s_bits[16];
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6;
   const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
   const bool inside = px < v.W && py < v.H;
   const float pxf = (float)px, pyf = (float)py;
@@ -89,43 +91,54 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
   const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
 
   float T = 1.0f;
-  uint32_t contributor = 0, last = 0;
+  uint32_t last = 0;
   float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  int todo = n;
-  for (int r = 0; r < rounds; ++r, todo -= TILE_PIX) {
+  for (int r = 0; r < rounds; ++r) {
     const int num_done = __syncthreads_count(done);
     if (num_done == TILE_PIX) break;
     const int k = r * TILE_PIX + tid;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
     if (k < n) {
       const uint32_t gidx = point_list[range.x + k];
-      s_r0[tid] = rec[3 * (int64_t)gidx + 0];
+      r0 = rec[3 * (int64_t)gidx + 0];
+      s_r0[tid] = r0;
       s_r1[tid] = rec[3 * (int64_t)gidx + 1];
-      s_r2[tid] = rec[3 * (int64_t)gidx + 2];
+      r2 = rec[3 * (int64_t)gidx + 2];
+      s_r2[tid] = make_float2(r2.x, r2.y);
     }
+    publish_strip_masks(k < n, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
     __syncthreads();
-    const int cnt = min(TILE_PIX, todo);
-    for (int j = 0; !done && j < cnt; ++j) {
-      ++contributor;
-      const float4 a = s_r0[j];
-      const float4 b = s_r1[j];
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, b.y * gexp(power));
-      if (alpha < 1.0f / 255.0f) continue;
-      const float test_T = T * (1.0f - alpha);
-      if (test_T < 0.0001f) {
-        done = true;
-        continue;
+    // this wave visits, in list order, only the batch elements whose alpha box reaches its strip
+    bool wave_live = __ballot(!done) != 0ull;
+    for (int c = 0; c < 4 && wave_live; ++c) {
+      uint64_t bits = wave_bits(s_bits, w, c);
+      while (bits != 0ull && wave_live) {
+        const int j = 64 * c + (int)__builtin_ctzll(bits);
+        bits &= bits - 1ull;
+        if (!done) {
+          const float4 a = s_r0[j];
+          const float4 b = s_r1[j];
+          const float dx = a.x - pxf, dy = a.y - pyf;
+          const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+          const float alpha = fminf(0.99f, b.y * gexp(power));
+          if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+            const float test_T = T * (1.0f - alpha);
+            if (test_T < 0.0001f) {
+              done = true;
+            } else {
+              const float2 cc = s_r2[j];
+              const float wt = alpha * T;
+              C0 += b.z * wt;
+              C1 += b.w * wt;
+              C2 += cc.x * wt;
+              Dp += cc.y * wt;
+              T = test_T;
+              last = (uint32_t)(k - tid + j + 1);  // 1-based list position
+            }
+          }
+        }
+        wave_live = __ballot(!done) != 0ull;
       }
-      const float4 c = s_r2[j];
-      const float w = alpha * T;
-      C0 += b.z * w;
-      C1 += b.w * w;
-      C2 += c.x * w;
-      Dp += c.y * w;
-      T = test_T;
-      last = contributor;
     }
   }
   if (inside) {

@@ -47,9 +47,79 @@ struct PreOut {
   float rgb[3];
   float depth;
   uint32_t clamped;
+  uint32_t ext;  // packed half-extents (1/8 px units) of the alpha >= 1/255 ellipse's bounding box
   int radius;
   int rmin_x, rmin_y, rmax_x, rmax_y;
 };
+
+// Conservative bounding box of the pixels that can pass the alpha >= 1/255 test, packed as two u16
+// half-extents in 1/8 px (0xFFFF = unbounded).  Used by the tile passes to skip a Gaussian for a whole
+// wave when no pixel of the wave's 16x4 strip can blend it: the skipped lanes would all fail the
+// alpha test, so results are bit-identical with and without the cull.
+//
+// Exact math: alpha >= 1/255  <=>  Q(d) = A dx^2 + C dy^2 + 2 B dx dy <= t = 2 ln(255 o).  The float
+// evaluation of Q in the tile passes has absolute error <= e |d|^2 with e = 32 eps (A + C) (each
+// term carries a few roundings and |2 B dx dy| <= max(A, C) |d|^2), so every accepted pixel lies in
+// {d : d^T (Q - e I) d <= t}, whose half-extents are sqrt(t (Q - e I)^-1_ii) -- computed in double
+// from the *stored* conic.  A 2 % margin on t covers exp/log error; +0.1 px covers the box test.
+// Needle-like splats for which Q - e I is not positive definite get an unbounded box.
+__device__ __forceinline__ uint32_t alpha_extent(float op_eff, float A, float B, float C) {
+  if (!(op_eff * 255.0f > 1.0f)) return 0u;  // alpha = o G <= o < 1/255 everywhere: never blended
+  const double t = 2.0 * log(255.0 * (double)op_eff) * 1.02 + 1e-6;
+  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
+  const double a = (double)A - e, c = (double)C - e;
+  const double det = a * c - (double)B * (double)B;
+  if (!(a > 0.0 && c > 0.0 && det > 0.0)) return 0xFFFFFFFFu;
+  const double ex = sqrt(t * c / det) + 0.1, ey = sqrt(t * a / det) + 0.1;
+  const uint32_t qx = (uint32_t)fmin(65535.0, ceil(ex * 8.0));
+  const uint32_t qy = (uint32_t)fmin(65535.0, ceil(ey * 8.0));
+  return qx | (qy << 16);
+}
+
+// Strip mask of a Gaussian in tile (tile_x, tile_y): bit s set when its alpha box can reach strip s =
+// tile rows 4s..4s+3 (all 16 columns) -- the pixels of wave s in the 256-thread tile passes.
+__device__ __forceinline__ uint32_t strip_mask4(float gx, float gy, uint32_t ext, int tile_x, int tile_y) {
+#ifdef GSLM_NO_STRIP_CULL
+  return 0xFu;
+#endif
+  const uint32_t qx = ext & 0xFFFFu, qy = ext >> 16;
+  const float ex = qx == 0xFFFFu ? INFINITY : (float)qx * 0.125f;
+  const float ey = qy == 0xFFFFu ? INFINITY : (float)qy * 0.125f;
+  const float x0 = (float)(tile_x * TILE_X), y0 = (float)(tile_y * TILE_Y);
+  if (!(fabsf(gx - fminf(fmaxf(gx, x0), x0 + (TILE_X - 1))) <= ex)) return 0u;
+  uint32_t m = 0u;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float ys = y0 + 4.0f * s;
+    if (fabsf(gy - fminf(fmaxf(gy, ys), ys + 3.0f)) <= ey) m |= 1u << s;
+  }
+  return m;
+}
+
+// Called by all 256 threads after thread tid has fetched batch element tid (`valid`: tid < cnt).
+// Publishes, per strip s, the 256-bit set of batch elements that can touch it: s_bits[4 s + c] holds
+// elements 64c..64c+63.  Wave s then visits only those elements (wave_bits / s_ff1), skipping the
+// rest for the whole wave: every skipped lane would have failed the alpha test, so the pass's
+// results are bit-identical to visiting every element.  Returns this element's own mask.
+__device__ __forceinline__ uint32_t publish_strip_masks(bool valid, float gx, float gy, uint32_t ext, int tile_x,
+                                                        int tile_y, uint64_t* s_bits) {
+  const uint32_t m = valid ? strip_mask4(gx, gy, ext, tile_x, tile_y) : 0u;
+  const int c = threadIdx.x >> 6;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint64_t b = __ballot((m >> s) & 1u);
+    if ((threadIdx.x & 63) == 0) s_bits[4 * s + c] = b;
+  }
+  return m;
+}
+
+// The 64-element hit set c of strip (wave) s as a wave-uniform (SGPR) value.
+__device__ __forceinline__ uint64_t wave_bits(const uint64_t* s_bits, int s, int c) {
+  const uint64_t b = s_bits[4 * s + c];
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // Activated scale / rotation of Gaussian i (fusing exp / normalize when RAW).
 template <bool RAW>
@@ -135,6 +205,7 @@ __device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, 
   o.opac = op * h;
   o.depth = tz;
   o.radius = (int)radius;
+  o.ext = alpha_extent(o.opac, o.conic[0], o.conic[1], o.conic[2]);
   return true;
 }
 

@@ -60,6 +60,24 @@ __device__ __forceinline__ float wave_reduce8_t(const float v[8], int lane) {
   return x;                 // value index of this lane: (lane >> 3) & 7
 }
 
+// Block-wide count of `pred` over 256 threads (4 waves) with one barrier; s_cnt = 4 ints of LDS the
+// caller owns.  Replaces __syncthreads_count, whose lowering reserves 256 B of LDS per block -- the
+// difference between 3 and 4 resident blocks per CU for k_render_matvec.  Safe to call once per
+// round as long as another barrier separates consecutive calls (the batch-load barrier does).
+__device__ __forceinline__ int block_count(bool pred, int* s_cnt) {
+  const uint64_t b = __ballot(pred);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = __popcll(b);
+  __syncthreads();
+  return (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+}
+
+// Wave-wide max of a non-negative int (all lanes active); every lane gets the result.
+__device__ __forceinline__ int wave_max_u(int x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o));
+  return x;
+}
+
 // Screen-space gradient of one (tile, Gaussian) pair, value index q:
 //   0 dL/dx_pix  1 dL/dy_pix  2 dL/dconic.a  3 dL/dconic.b  4 dL/dconic.c  5 dL/dopacity_eff
 //   6..8 dL/drgb  9 dL/dinvdepth
@@ -143,15 +161,17 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
                                          uint2 range, const uint32_t* __restrict__ point_list,
                                          const float4* __restrict__ rec, const uint2* __restrict__ rect,
                                          const uint32_t* __restrict__ goff, float4* s_r0, float4* s_r1,
-                                         float4* s_r2, float* s_acc, int* s_misc, float4* __restrict__ rows) {
+                                         float2* s_r2, uint64_t* s_bits, float* s_acc, int* s_misc,
+                                         float4* __restrict__ rows) {
   constexpr int NU = n_used<WITH_XY, WITH_INV>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // Positions >= max over pixels of n_contrib are never blended: their rows are zero.
-  if (tid == 0) s_misc[0] = 0;
+  // Positions >= max over pixels of n_contrib are never blended: their rows are zero.  The leading
+  // barrier lets s_misc alias LDS the caller used before this pass (k_render_matvec's JVP buffers).
   __syncthreads();
-  if (st.last) atomicMax(&s_misc[0], (int)st.last);
+  const int wmax = wave_max_u((int)st.last);
+  if (lane == 0) s_misc[w] = wmax;
   __syncthreads();
-  const int n_eff = s_misc[0];
+  const int n_eff = max(max(s_misc[0], s_misc[1]), max(s_misc[2], s_misc[3]));
   {
     float z[NV];
 #pragma unroll
@@ -162,93 +182,103 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     }
   }
   const int rounds = (n_eff + TILE_PIX - 1) / TILE_PIX;
-  uint32_t contributor = (uint32_t)n_eff;
   for (int r = 0; r < rounds; ++r) {
     const int base = n_eff - 1 - r * TILE_PIX;  // list position of batch element 0
     const int cnt = min(TILE_PIX, base + 1);
     __syncthreads();
     uint32_t my_slot = 0;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
     if (tid < cnt) {
       const uint32_t g = point_list[range.x + base - tid];
-      s_r0[tid] = rec[3 * (int64_t)g + 0];
+      r0 = rec[3 * (int64_t)g + 0];
+      r2 = rec[3 * (int64_t)g + 2];
+      s_r0[tid] = r0;
       s_r1[tid] = rec[3 * (int64_t)g + 1];
-      s_r2[tid] = rec[3 * (int64_t)g + 2];
+      s_r2[tid] = make_float2(r2.x, r2.y);
       my_slot = row_slot(goff[g], rect[g], tile_x, tile_y);
     }
+    // which waves' strips this element can touch; wave w visits only its hits, and the combine below
+    // takes zero for the others (exactly what a visit with no valid lane would have produced)
+    const uint32_t my_mask = publish_strip_masks(tid < cnt, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
     __syncthreads();
-    for (int j = 0; j < cnt; ++j) {
-      --contributor;
-      const float4 a = s_r0[j];
-      const float4 b = s_r1[j];
-      const float4 c = s_r2[j];
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      const float G = gexp(power);
-      const float alpha = fminf(0.99f, b.y * G);
-      const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
-      float gv[NV];
+    for (int cc = 0; cc < 4; ++cc) {
+      uint64_t bits = wave_bits(s_bits, w, cc);
+      while (bits != 0ull) {
+        const int j = 64 * cc + (int)__builtin_ctzll(bits);
+        bits &= bits - 1ull;
+        const uint32_t contributor = (uint32_t)(base - j);  // 0-based list position
+        const float4 a = s_r0[j];
+        const float4 b = s_r1[j];
+        const float2 c = s_r2[j];
+        const float dx = a.x - pxf, dy = a.y - pyf;
+        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float G = gexp(power);
+        const float alpha = fminf(0.99f, b.y * G);
+        const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
+        float gv[NV];
 #pragma unroll
-      for (int q = 0; q < NV; ++q) gv[q] = 0.f;
-      if (valid) {
-        const float inv1ma = rcp_f(1.f - alpha);
-        st.T = st.T * inv1ma;
-        const float dchannel = alpha * st.T;
-        const float col[3] = {b.z, b.w, c.x};
-        float dL_dalpha = 0.f;
+        for (int q = 0; q < NV; ++q) gv[q] = 0.f;
+        if (valid) {
+          const float inv1ma = rcp_f(1.f - alpha);
+          st.T = st.T * inv1ma;
+          const float dchannel = alpha * st.T;
+          const float col[3] = {b.z, b.w, c.x};
+          float dL_dalpha = 0.f;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-          st.acc[ch] = st.last_alpha * st.last_color[ch] + (1.f - st.last_alpha) * st.acc[ch];
-          st.last_color[ch] = col[ch];
-          dL_dalpha += (col[ch] - st.acc[ch]) * st.dpix[ch];
-          gv[6 + ch] = dchannel * st.dpix[ch];
+          for (int ch = 0; ch < 3; ++ch) {
+            st.acc[ch] = st.last_alpha * st.last_color[ch] + (1.f - st.last_alpha) * st.acc[ch];
+            st.last_color[ch] = col[ch];
+            dL_dalpha += (col[ch] - st.acc[ch]) * st.dpix[ch];
+            gv[6 + ch] = dchannel * st.dpix[ch];
+          }
+          if (WITH_INV) {
+            const float invd = c.y;
+            st.acc_inv = st.last_alpha * st.last_inv + (1.f - st.last_alpha) * st.acc_inv;
+            st.last_inv = invd;
+            dL_dalpha += (invd - st.acc_inv) * st.dinv;
+            gv[9] = dchannel * st.dinv;
+          }
+          dL_dalpha *= st.T;
+          st.last_alpha = alpha;
+          dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
+          const float dL_dG = b.y * dL_dalpha;
+          const float gdx = G * dx, gdy = G * dy;
+          if (WITH_XY) {
+            gv[0] = dL_dG * (-gdx * a.z - gdy * a.w);
+            gv[1] = dL_dG * (-gdy * b.x - gdx * a.w);
+          }
+          gv[2] = -0.5f * gdx * dx * dL_dG;
+          gv[3] = -gdx * dy * dL_dG;
+          gv[4] = -0.5f * gdy * dy * dL_dG;
+          gv[5] = G * dL_dalpha;
         }
-        if (WITH_INV) {
-          const float invd = c.y;
-          st.acc_inv = st.last_alpha * st.last_inv + (1.f - st.last_alpha) * st.acc_inv;
-          st.last_inv = invd;
-          dL_dalpha += (invd - st.acc_inv) * st.dinv;
-          gv[9] = dchannel * st.dinv;
-        }
-        dL_dalpha *= st.T;
-        st.last_alpha = alpha;
-        dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
-        const float dL_dG = b.y * dL_dalpha;
-        const float gdx = G * dx, gdy = G * dy;
-        if (WITH_XY) {
-          gv[0] = dL_dG * (-gdx * a.z - gdy * a.w);
-          gv[1] = dL_dG * (-gdy * b.x - gdx * a.w);
-        }
-        gv[2] = -0.5f * gdx * dx * dL_dG;
-        gv[3] = -gdx * dy * dL_dG;
-        gv[4] = -0.5f * gdy * dy * dL_dG;
-        gv[5] = G * dL_dalpha;
-      }
-      const bool any = __ballot(valid) != 0ull;
-      if constexpr (NU <= 8) {
-        // transposed reduction: value slot k ends in lanes 8k..8k+7; lane 8k stores it
-        float r = 0.f;
-        if (any) {
-          float pv[8];
+        const bool any = __ballot(valid) != 0ull;
+        if constexpr (NU <= 8) {
+          // transposed reduction: value slot k ends in lanes 8k..8k+7; lane 8k stores it
+          float rr = 0.f;
+          if (any) {
+            float pv[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) pv[k] = 0.f;
+            for (int k = 0; k < 8; ++k) pv[k] = 0.f;
 #pragma unroll
-          for (int q = 0; q < NV; ++q)
-            if (q_used<WITH_XY, WITH_INV>(q)) pv[q_slot<WITH_XY, WITH_INV>(q)] = gv[q];
-          r = wave_reduce8_t(pv, lane);
-        }
-        const int k = lane >> 3;
-        if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * TILE_PIX + j] = r;
-      } else {
-        if (any) {
+            for (int q = 0; q < NV; ++q)
+              if (q_used<WITH_XY, WITH_INV>(q)) pv[q_slot<WITH_XY, WITH_INV>(q)] = gv[q];
+            rr = wave_reduce8_t(pv, lane);
+          }
+          const int k = lane >> 3;
+          if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * TILE_PIX + j] = rr;
+        } else {
+          if (any) {
 #pragma unroll
-          for (int q = 0; q < NV; ++q)
-            if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
-        }
-        if (lane == 63) {
+            for (int q = 0; q < NV; ++q)
+              if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
+          }
+          if (lane == 63) {
 #pragma unroll
-          for (int q = 0; q < NV; ++q)
-            if (q_used<WITH_XY, WITH_INV>(q))
-              s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
+            for (int q = 0; q < NV; ++q)
+              if (q_used<WITH_XY, WITH_INV>(q))
+                s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
+          }
         }
       }
     }
@@ -260,8 +290,11 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         t[q] = 0.f;
         if (q_used<WITH_XY, WITH_INV>(q)) {
           const int sq = q_slot<WITH_XY, WITH_INV>(q);
-          t[q] = ((s_acc[(0 * NU + sq) * TILE_PIX + tid] + s_acc[(1 * NU + sq) * TILE_PIX + tid]) +
-                  s_acc[(2 * NU + sq) * TILE_PIX + tid]) + s_acc[(3 * NU + sq) * TILE_PIX + tid];
+          const float p0 = (my_mask & 1u) ? s_acc[(0 * NU + sq) * TILE_PIX + tid] : 0.f;
+          const float p1 = (my_mask & 2u) ? s_acc[(1 * NU + sq) * TILE_PIX + tid] : 0.f;
+          const float p2 = (my_mask & 4u) ? s_acc[(2 * NU + sq) * TILE_PIX + tid] : 0.f;
+          const float p3 = (my_mask & 8u) ? s_acc[(3 * NU + sq) * TILE_PIX + tid] : 0.f;
+          t[q] = ((p0 + p1) + p2) + p3;
         }
       }
       store_row<ROWF4>(rows, my_slot, t);

@@ -31,13 +31,16 @@ struct JvpPix {
   float T, dT, dC[3], dD;
 };
 
-// Front-to-back tangent pass over the tile.  Block-uniform; blockDim = 256.
+// Front-to-back tangent pass over the tile.  Block-uniform; blockDim = 256.  Wave w visits only the
+// batch elements whose alpha box reaches its 16x4 strip (publish_strip_masks); the stop decision is
+// frozen at the primal (`last` = n_contrib).
 template <bool WITH_XY, bool WITH_INV>
-__device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, float pyf, uint32_t last, uint2 range,
-                                         const uint32_t* __restrict__ point_list, const float4* __restrict__ rec,
-                                         const float4* __restrict__ trec, float4* s_r0, float4* s_r1, float4* s_r2,
-                                         float4* s_t0, float4* s_t1, float4* s_t2) {
-  const int tid = threadIdx.x;
+__device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, float pyf, int tile_x, int tile_y,
+                                         uint32_t last, uint2 range, const uint32_t* __restrict__ point_list,
+                                         const float4* __restrict__ rec, const float4* __restrict__ trec,
+                                         float4* s_r0, float4* s_r1, float2* s_r2, float4* s_t0, float4* s_t1,
+                                         float2* s_t2, uint64_t* s_bits, int* s_cnt) {
+  const int tid = threadIdx.x, w = tid >> 6;
   o.T = 1.f;
   o.dT = 0.f;
   o.dC[0] = o.dC[1] = o.dC[2] = 0.f;
@@ -45,55 +48,61 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
   bool done = !inside || last == 0;
   const int n = (int)(range.y - range.x);
   const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
-  uint32_t contributor = 0;
-  int todo = n;
-  for (int r = 0; r < rounds; ++r, todo -= TILE_PIX) {
-    const int num_done = __syncthreads_count(done);
+  for (int r = 0; r < rounds; ++r) {
+    const int num_done = block_count(done, s_cnt);
     if (num_done == TILE_PIX) break;
     const int k = r * TILE_PIX + tid;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
     if (k < n) {
       const uint32_t g = point_list[range.x + k];
-      s_r0[tid] = rec[3 * (int64_t)g + 0];
+      r0 = rec[3 * (int64_t)g + 0];
+      r2 = rec[3 * (int64_t)g + 2];
+      s_r0[tid] = r0;
       s_r1[tid] = rec[3 * (int64_t)g + 1];
-      s_r2[tid] = rec[3 * (int64_t)g + 2];
+      s_r2[tid] = make_float2(r2.x, r2.y);
       s_t0[tid] = trec[3 * (int64_t)g + 0];
       s_t1[tid] = trec[3 * (int64_t)g + 1];
-      s_t2[tid] = trec[3 * (int64_t)g + 2];
+      const float4 t2 = trec[3 * (int64_t)g + 2];
+      s_t2[tid] = make_float2(t2.x, t2.y);
     }
+    publish_strip_masks(k < n, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
     __syncthreads();
-    const int cnt = min(TILE_PIX, todo);
-    for (int j = 0; !done && j < cnt; ++j) {
-      ++contributor;
-      const float4 a = s_r0[j];
-      const float4 b = s_r1[j];
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      const float G = gexp(power);
-      const float alpha = fminf(0.99f, b.y * G);
-      if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-        const float4 c = s_r2[j];
-        const float4 t0 = s_t0[j];
-        const float4 t1 = s_t1[j];
-        float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
-        if (WITH_XY) {
-          const float ddx = t0.x, ddy = t0.y;
-          dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
+    bool wave_live = __ballot(!done) != 0ull;
+    for (int c = 0; c < 4 && wave_live; ++c) {
+      uint64_t bits = wave_bits(s_bits, w, c);
+      while (bits != 0ull && wave_live) {
+        const int j = 64 * c + (int)__builtin_ctzll(bits);
+        bits &= bits - 1ull;
+        if (!done) {
+          const float4 a = s_r0[j];
+          const float4 b = s_r1[j];
+          const float dx = a.x - pxf, dy = a.y - pyf;
+          const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+          const float G = gexp(power);
+          const float alpha = fminf(0.99f, b.y * G);
+          if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+            const float2 cc = s_r2[j];
+            const float4 t0 = s_t0[j];
+            const float4 t1 = s_t1[j];
+            const float2 t2 = s_t2[j];
+            float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
+            if (WITH_XY) {
+              const float ddx = t0.x, ddy = t0.y;
+              dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
+            }
+            const float dalpha = G * (t1.y + b.y * dpower);
+            const float wt = alpha * o.T;
+            const float dw = dalpha * o.T + alpha * o.dT;
+            o.dC[0] += t1.z * wt + b.z * dw;
+            o.dC[1] += t1.w * wt + b.w * dw;
+            o.dC[2] += t2.x * wt + cc.x * dw;
+            if (WITH_INV) o.dD += t2.y * wt + cc.y * dw;
+            o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
+            o.T = o.T * (1.f - alpha);
+            if ((uint32_t)(k - tid + j + 1) == last) done = true;
+          }
         }
-        const float dalpha = G * (t1.y + b.y * dpower);
-        const float w = alpha * o.T;
-        const float dw = dalpha * o.T + alpha * o.dT;
-        o.dC[0] += t1.z * w + b.z * dw;
-        o.dC[1] += t1.w * w + b.w * dw;
-        if (WITH_INV) {
-          const float4 t2 = s_t2[j];
-          o.dC[2] += t2.x * w + c.x * dw;
-          o.dD += t2.y * w + c.y * dw;
-        } else {
-          o.dC[2] += s_t2[j].x * w + c.x * dw;
-        }
-        o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
-        o.T = o.T * (1.f - alpha);
-        if (contributor == last) done = true;
+        wave_live = __ballot(!done) != 0ull;
       }
     }
   }
@@ -105,8 +114,10 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
                                                      const float4* __restrict__ rec, const float4* __restrict__ trec,
                                                      const uint32_t* __restrict__ n_contrib,
                                                      float* __restrict__ out_color_t, float* __restrict__ out_inv_t) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_r2[TILE_PIX];
-  __shared__ float4 s_t0[TILE_PIX], s_t1[TILE_PIX], s_t2[TILE_PIX];
+  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_t0[TILE_PIX], s_t1[TILE_PIX];
+  __shared__ float2 s_r2[TILE_PIX], s_t2[TILE_PIX];
+  __shared__ uint64_t s_bits[16];
+  __shared__ int s_cnt[4];
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
@@ -115,8 +126,8 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   const int64_t pid = (int64_t)py * v.W + px;
   const uint32_t last = inside ? n_contrib[pid] : 0u;
   JvpPix o;
-  jvp_tile<WITH_XY, true>(o, inside, (float)px, (float)py, last, ranges[tile], point_list, rec, trec, s_r0, s_r1,
-                          s_r2, s_t0, s_t1, s_t2);
+  jvp_tile<WITH_XY, true>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec, trec,
+                          s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   if (inside) {
     const int64_t HW = (int64_t)v.H * v.W;
     out_color_t[pid] = o.dC[0] + o.dT * v.bg[0];
@@ -136,10 +147,22 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
                                                         const float* __restrict__ final_T,
                                                         const uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ weight, float4* __restrict__ contrib) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_r2[TILE_PIX];
-  __shared__ float4 s_t0[TILE_PIX], s_t1[TILE_PIX], s_t2[TILE_PIX];
-  __shared__ float s_acc[vjp_acc_floats<WITH_XY, false>()];
-  __shared__ int s_misc[4];
+  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
+  __shared__ float2 s_r2[TILE_PIX];
+  __shared__ uint64_t s_bits[16];
+  __shared__ int s_cnt[4];
+  // The JVP pass's tangent records and the VJP pass's per-wave partials (+ its n_eff scratch) are
+  // never live together (vjp_tile starts with a block barrier): one LDS region.
+  // LM path: 10 KB + 28 KB (+ 10 KB records, masks) = 38.1 KB per block -> 4 blocks per CU.
+  constexpr int kAcc = vjp_acc_floats<WITH_XY, false>();
+  constexpr int kTan = (4 + 4 + 2) * TILE_PIX;
+  static_assert(kAcc >= kTan, "tangent records fit in the partial-sum region");
+  __shared__ float4 s_union[kAcc / 4];
+  float4* s_t0 = s_union;
+  float4* s_t1 = s_union + TILE_PIX;
+  float2* s_t2 = reinterpret_cast<float2*>(s_union + 2 * TILE_PIX);
+  float* s_acc = reinterpret_cast<float*>(s_union);
+  int* s_misc = reinterpret_cast<int*>(s_union);
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
@@ -158,8 +181,8 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
     w2 = weight[2 * HW + pid];
   }
   JvpPix o;
-  jvp_tile<WITH_XY, false>(o, inside, (float)px, (float)py, last, range, point_list, rec, trec, s_r0, s_r1, s_r2,
-                           s_t0, s_t1, s_t2);
+  jvp_tile<WITH_XY, false>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
+                           s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   // u = 2 * w (.) (J v)   -- factor 2: the [r; r] residual aliasing of batch_training_loss.py:17
   const float u0 = 2.f * w0 * (o.dC[0] + o.dT * v.bg[0]);
   const float u1 = 2.f * w1 * (o.dC[1] + o.dT * v.bg[1]);
@@ -167,7 +190,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
-                                            rect, goff, s_r0, s_r1, s_r2, s_acc, s_misc, contrib);
+                                            rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib);
 }
 
 // ------------------------------------------------------------------ launchers
