@@ -105,12 +105,13 @@ static int make_view(const gslm_view* in, int M, ViewK* v) {
   v->D = in->sh_degree;
   v->M = M;
   v->antialiasing = in->antialiasing ? 1 : 0;
+  v->exhaustive = in->debug ? 1 : 0;
   return GSLM_OK;
 }
 
 static int make_gauss(const gslm_gaussians* in, const ViewK* v, GaussK* g, bool tangent) {
   if (!in) { set_error("gaussians is NULL"); return GSLM_ERR_INVALID; }
-  if (in->P < 0 || in->P > 0x7FFFFFFFll) { set_error("P out of range"); return GSLM_ERR_INVALID; }
+  if (in->P < 0 || in->P > MAX_P) { set_error("P out of range [0, 2^28 - 1]"); return GSLM_ERR_INVALID; }
   g->P = in->P;
   g->raw = in->raw ? 1 : 0;
   g->M = in->max_coeffs;
@@ -368,7 +369,10 @@ int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, in
   bin_layout(N, ntiles, const_cast<void*>(binning), &bb);
   img_layout(H, W, const_cast<void*>(image), &ib);
   const auto D2D = hipMemcpyDeviceToDevice;
-  if (point_list && N) GSLM_HIP_CHECK(hipMemcpyAsync(point_list, bb.point_list, (size_t)N * 4, D2D, s));
+  if (point_list && N) {
+    const int st = launch_point_ids(bb.point_list, N, point_list, s);
+    if (st) return st;
+  }
   if (ranges && binning) GSLM_HIP_CHECK(hipMemcpyAsync(ranges, bb.ranges, (size_t)ntiles * 8, D2D, s));
   if (tiles_touched && P) GSLM_HIP_CHECK(hipMemcpyAsync(tiles_touched, gb.tiles, (size_t)P * 4, D2D, s));
   if (final_T && image) GSLM_HIP_CHECK(hipMemcpyAsync(final_T, ib.final_T, (size_t)H * W * 4, D2D, s));

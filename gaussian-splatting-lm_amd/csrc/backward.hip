@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
-  const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
   const bool inside = px < v.W && py < v.H;
   const int64_t pid = (int64_t)py * v.W + px;
   const int64_t HW = (int64_t)v.H * v.W;

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
 
   const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
   const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
-  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), __uint_as_float(o.ext));
+  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.tq);
   rec[3 * i + 0] = r0;
   rec[3 * i + 1] = r1;
   rec[3 * i + 2] = r2;
@@ -43,8 +43,8 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                     const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ tiles,
-                                                    const uint2* __restrict__ rect, uint32_t* __restrict__ keys,
-                                                    uint32_t* __restrict__ vals) {
+                                                    const uint2* __restrict__ rect, const float4* __restrict__ rec,
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= P) return;
   const uint32_t g = sorted_idx[s];
@@ -53,12 +53,20 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   uint32_t off = offsets[s];
   const uint2 rc = rect[g];
   const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
+  const float4 r0 = rec[3 * (int64_t)g + 0];
+  const float C = rec[3 * (int64_t)g + 1].x, tq = rec[3 * (int64_t)g + 2].w;
   for (int ty = y0; ty < y1; ++ty)
     for (int tx = x0; tx < x1; ++tx) {
       keys[off] = (uint32_t)(ty * gx + tx);
-      vals[off] = g;
+      vals[off] = g | (quad_mask4(r0.x, r0.y, r0.z, r0.w, C, tq, tx, ty) << ID_BITS);
       ++off;
     }
+}
+
+// Gaussian ids of the sorted list (mask bits stripped), for gslm_inspect.
+__global__ __launch_bounds__(256) void k_point_ids(int64_t N, const uint32_t* __restrict__ pl, uint32_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < N) out[k] = pl_id(pl[k]);
 }
 
 __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __restrict__ keys,
@@ -70,7 +78,7 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
   if (k == N - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
 }
 
-// renderCUDA forward.  Pixel (px,py) of the tile is thread ty*16+tx: wave w holds rows 4w..4w+3.
+// renderCUDA forward.  Wave w holds the tile's 8x8 quadrant w (tile_pixel).
 __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
                                                      const float4* __restrict__ rec, float* __restrict__ out_color,
@@ -82,7 +90,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x, w = tid >> 6;
-  const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
   const bool inside = px < v.W && py < v.H;
   const float pxf = (float)px, pyf = (float)py;
   bool done = !inside;
@@ -97,18 +106,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
     const int num_done = __syncthreads_count(done);
     if (num_done == TILE_PIX) break;
     const int k = r * TILE_PIX + tid;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
+    uint32_t m = 0u;
     if (k < n) {
-      const uint32_t gidx = point_list[range.x + k];
-      r0 = rec[3 * (int64_t)gidx + 0];
-      s_r0[tid] = r0;
-      s_r1[tid] = rec[3 * (int64_t)gidx + 1];
-      r2 = rec[3 * (int64_t)gidx + 2];
+      const uint32_t e = point_list[range.x + k];
+      const int64_t gidx = pl_id(e);
+      m = pl_mask(e);
+      s_r0[tid] = rec[3 * gidx + 0];
+      s_r1[tid] = rec[3 * gidx + 1];
+      const float4 r2 = rec[3 * gidx + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
     }
-    publish_strip_masks(k < n, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
+    publish_quad_masks(m, s_bits);
     __syncthreads();
-    // this wave visits, in list order, only the batch elements whose alpha box reaches its strip
+    // this wave visits, in list order, only the batch elements whose alpha region reaches its quadrant
     bool wave_live = __ballot(!done) != 0ull;
     for (int c = 0; c < 4 && wave_live; ++c) {
       uint64_t bits = wave_bits(s_bits, w, c);
@@ -172,7 +182,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0)
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
-                       gb.offsets, gb.tiles, gb.rect, bb.keys0, bb.vals0);
+                       gb.offsets, gb.tiles, gb.rect, gb.rec, bb.keys0, bb.vals0);
   GSLM_LAUNCH_CHECK();
   if (N == 0) return GSLM_OK;
   bool alt = false;
@@ -184,6 +194,13 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   }
   const unsigned nbN = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s) {
+  if (N <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_point_ids, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, point_list, out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -35,6 +35,7 @@ struct ViewK {
   int D;                                 // active SH degree
   int M;                                 // SH coefficients stored per Gaussian
   int antialiasing;
+  int exhaustive;                        // gslm_view.debug: disable the quadrant cull (reference traversal)
 };
 
 // transformPoint4x3 / 4x4, one row at a time (same association as the oracle)

@@ -47,73 +47,102 @@ struct PreOut {
   float rgb[3];
   float depth;
   uint32_t clamped;
-  uint32_t ext;  // packed half-extents (1/8 px units) of the alpha >= 1/255 ellipse's bounding box
+  float tq;  // alpha threshold of the quadrant cull (alpha_threshold), stored in the record's r2.w
   int radius;
   int rmin_x, rmin_y, rmax_x, rmax_y;
 };
 
-// Conservative bounding box of the pixels that can pass the alpha >= 1/255 test, packed as two u16
-// half-extents in 1/8 px (0xFFFF = unbounded).  Used by the tile passes to skip a Gaussian for a whole
-// wave when no pixel of the wave's 16x4 strip can blend it: the skipped lanes would all fail the
-// alpha test, so results are bit-identical with and without the cull.
+// ---------------- quadrant culling (an exact-results skip, not an approximation) ----------------
+// A 16x16 tile pass runs one wave per 8x8 quadrant (tile_pixel).  For every batch element the block
+// computes which quadrants its alpha >= 1/255 region can reach, and each wave visits only those
+// elements.  A skipped lane would have failed the alpha test, so results are bit-identical to
+// visiting every element; only wasted iterations go.
 //
-// Exact math: alpha >= 1/255  <=>  Q(d) = A dx^2 + C dy^2 + 2 B dx dy <= t = 2 ln(255 o).  The float
-// evaluation of Q in the tile passes has absolute error <= e |d|^2 with e = 32 eps (A + C) (each
-// term carries a few roundings and |2 B dx dy| <= max(A, C) |d|^2), so every accepted pixel lies in
-// {d : d^T (Q - e I) d <= t}, whose half-extents are sqrt(t (Q - e I)^-1_ii) -- computed in double
-// from the *stored* conic.  A 2 % margin on t covers exp/log error; +0.1 px covers the box test.
-// Needle-like splats for which Q - e I is not positive definite get an unbounded box.
-__device__ __forceinline__ uint32_t alpha_extent(float op_eff, float A, float B, float C) {
-  if (!(op_eff * 255.0f > 1.0f)) return 0u;  // alpha = o G <= o < 1/255 everywhere: never blended
-  const double t = 2.0 * log(255.0 * (double)op_eff) * 1.02 + 1e-6;
-  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
-  const double a = (double)A - e, c = (double)C - e;
-  const double det = a * c - (double)B * (double)B;
-  if (!(a > 0.0 && c > 0.0 && det > 0.0)) return 0xFFFFFFFFu;
-  const double ex = sqrt(t * c / det) + 0.1, ey = sqrt(t * a / det) + 0.1;
-  const uint32_t qx = (uint32_t)fmin(65535.0, ceil(ex * 8.0));
-  const uint32_t qy = (uint32_t)fmin(65535.0, ceil(ey * 8.0));
-  return qx | (qy << 16);
+// Exact math: alpha >= 1/255  <=>  Q(d) = A dx^2 + C dy^2 + 2 B dx dy <= t = 2 ln(255 o), with
+// (A, B, C) the stored conic.  The float evaluation of Q in the tile passes (-ffp-contract=off, a
+// handful of roundings per term, |2 B dx dy| <= max(A, C) |d|^2) errs by at most 14 eps (A + C) |d|^2,
+// so every pixel a pass can accept satisfies d^T (Q - e I) d <= t with e = 32 eps (A + C).  The
+// quadrant test evaluates min over the quadrant of d^T (Q - e I) d in double and compares with
+// tq = t * 1.02 + 1e-4 (exp / log / 1/255-constant rounding), rounded up to float.
+
+// tq for effective opacity o; negative when o <= 1/255 (no pixel can ever pass).
+__device__ __forceinline__ float alpha_threshold(float op_eff) {
+  if (!(op_eff * 255.0f > 1.0f)) return -1.0f;
+  const double t = 2.0 * log(255.0 * (double)op_eff) * 1.02 + 1e-4;
+  float f = (float)t;  // t > 0: the next float up is the next bit pattern
+  if ((double)f < t) f = __uint_as_float(__float_as_uint(f) + 1u);
+  return f;
 }
 
-// Strip mask of a Gaussian in tile (tile_x, tile_y): bit s set when its alpha box can reach strip s =
-// tile rows 4s..4s+3 (all 16 columns) -- the pixels of wave s in the 256-thread tile passes.
-__device__ __forceinline__ uint32_t strip_mask4(float gx, float gy, uint32_t ext, int tile_x, int tile_y) {
+// min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of a x^2 + 2 b x y + c y^2,
+// for a, c > 0 and a c > b^2: 0 if the rectangle holds the centre, else attained on an edge.
+__device__ __forceinline__ double rect_qmin(double a, double b, double c, double x0, double x1, double y0, double y1) {
+  if (x0 <= 0.0 && x1 >= 0.0 && y0 <= 0.0 && y1 >= 0.0) return 0.0;
+  double best = INFINITY;
+  const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double xe = xs[k];
+    const double y = fmin(fmax(-b * xe / c, y0), y1);
+    best = fmin(best, (a * xe + 2.0 * b * y) * xe + c * y * y);
+    const double ye = ys[k];
+    const double x = fmin(fmax(-b * ye / a, x0), x1);
+    best = fmin(best, (c * ye + 2.0 * b * x) * ye + a * x * x);
+  }
+  return best;
+}
+
+// Quadrant mask of a Gaussian in tile (tile_x, tile_y): bit s set when its alpha region can reach
+// quadrant s = pixels [8 (s & 1), +7] x [8 (s >> 1), +7] of the tile (wave s).  NaN-safe: any NaN
+// input yields "reachable".
+__device__ __forceinline__ uint32_t quad_mask4(float gx, float gy, float A, float B, float C, float tq, int tile_x,
+                                               int tile_y) {
 #ifdef GSLM_NO_STRIP_CULL
   return 0xFu;
 #endif
-  const uint32_t qx = ext & 0xFFFFu, qy = ext >> 16;
-  const float ex = qx == 0xFFFFu ? INFINITY : (float)qx * 0.125f;
-  const float ey = qy == 0xFFFFu ? INFINITY : (float)qy * 0.125f;
-  const float x0 = (float)(tile_x * TILE_X), y0 = (float)(tile_y * TILE_Y);
-  if (!(fabsf(gx - fminf(fmaxf(gx, x0), x0 + (TILE_X - 1))) <= ex)) return 0u;
+  if (tq < 0.0f) return 0u;
+  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
+  const double a = (double)A - e, c = (double)C - e, b = (double)B;
+  if (!(a > 0.0 && c > 0.0 && a * c - b * b > 0.0)) return 0xFu;  // unbounded (or NaN) region
+  const double bx = (double)(tile_x * TILE_X) - (double)gx, by = (double)(tile_y * TILE_Y) - (double)gy;
   uint32_t m = 0u;
-#pragma unroll
+#pragma unroll 1
   for (int s = 0; s < 4; ++s) {
-    const float ys = y0 + 4.0f * s;
-    if (fabsf(gy - fminf(fmaxf(gy, ys), ys + 3.0f)) <= ey) m |= 1u << s;
+    const double x0 = bx + 8.0 * (s & 1), y0 = by + 8.0 * (s >> 1);
+    if (!(rect_qmin(a, b, c, x0, x0 + 7.0, y0, y0 + 7.0) > (double)tq)) m |= 1u << s;
   }
   return m;
 }
 
-// Called by all 256 threads after thread tid has fetched batch element tid (`valid`: tid < cnt).
-// Publishes, per strip s, the 256-bit set of batch elements that can touch it: s_bits[4 s + c] holds
-// elements 64c..64c+63.  Wave s then visits only those elements (wave_bits / s_ff1), skipping the
-// rest for the whole wave: every skipped lane would have failed the alpha test, so the pass's
-// results are bit-identical to visiting every element.  Returns this element's own mask.
-__device__ __forceinline__ uint32_t publish_strip_masks(bool valid, float gx, float gy, uint32_t ext, int tile_x,
-                                                        int tile_y, uint64_t* s_bits) {
-  const uint32_t m = valid ? strip_mask4(gx, gy, ext, tile_x, tile_y) : 0u;
+// point_list entries carry the Gaussian id in the low 28 bits and its quadrant mask (quad_mask4,
+// computed once per (tile, Gaussian) pair by k_duplicate) in the top 4 bits.
+constexpr int ID_BITS = 28;
+constexpr uint32_t ID_MASK = (1u << ID_BITS) - 1u;
+constexpr int64_t MAX_P = (int64_t)ID_MASK;  // 268M Gaussians per view and GPU
+__device__ __forceinline__ uint32_t pl_id(uint32_t e) { return e & ID_MASK; }
+__device__ __forceinline__ uint32_t pl_mask(uint32_t e) { return e >> ID_BITS; }
+
+// Pixel of thread tid in a 16x16 tile: wave w = tid >> 6 holds the 8x8 quadrant (w & 1, w >> 1).
+__device__ __forceinline__ void tile_pixel(int tile_x, int tile_y, int tid, int& px, int& py) {
+  const int w = tid >> 6, l = tid & 63;
+  px = tile_x * TILE_X + 8 * (w & 1) + (l & 7);
+  py = tile_y * TILE_Y + 8 * (w >> 1) + (l >> 3);
+}
+
+// Called by all 256 threads after thread tid has fetched batch element tid with quadrant mask m (0
+// when tid is past the batch).  Publishes, per quadrant s, the 256-bit set of batch elements that
+// can touch it: s_bits[4 s + c] holds elements 64c..64c+63.  Wave s then visits only those
+// elements, in list order (wave_bits / s_ff1).
+__device__ __forceinline__ void publish_quad_masks(uint32_t m, uint64_t* s_bits) {
   const int c = threadIdx.x >> 6;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const uint64_t b = __ballot((m >> s) & 1u);
     if ((threadIdx.x & 63) == 0) s_bits[4 * s + c] = b;
   }
-  return m;
 }
 
-// The 64-element hit set c of strip (wave) s as a wave-uniform (SGPR) value.
+// The 64-element hit set c of quadrant (wave) s as a wave-uniform (SGPR) value.
 __device__ __forceinline__ uint64_t wave_bits(const uint64_t* s_bits, int s, int c) {
   const uint64_t b = s_bits[4 * s + c];
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
@@ -205,7 +234,7 @@ __device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, 
   o.opac = op * h;
   o.depth = tz;
   o.radius = (int)radius;
-  o.ext = alpha_extent(o.opac, o.conic[0], o.conic[1], o.conic[2]);
+  o.tq = v.exhaustive ? INFINITY : alpha_threshold(o.opac);  // INFINITY: every quadrant visited
   return true;
 }
 
@@ -262,6 +291,7 @@ size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
 
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
 int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
+int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s);
 

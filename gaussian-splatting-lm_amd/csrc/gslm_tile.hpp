@@ -177,7 +177,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
 #pragma unroll
     for (int q = 0; q < NV; ++q) z[q] = 0.f;
     for (int64_t k = (int64_t)range.x + n_eff + tid; k < (int64_t)range.y; k += TILE_PIX) {
-      const uint32_t g = point_list[k];
+      const uint32_t g = pl_id(point_list[k]);
       store_row<ROWF4>(rows, row_slot(goff[g], rect[g], tile_x, tile_y), z);
     }
   }
@@ -187,19 +187,20 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     const int cnt = min(TILE_PIX, base + 1);
     __syncthreads();
     uint32_t my_slot = 0;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
+    uint32_t my_mask = 0u;
     if (tid < cnt) {
-      const uint32_t g = point_list[range.x + base - tid];
-      r0 = rec[3 * (int64_t)g + 0];
-      r2 = rec[3 * (int64_t)g + 2];
-      s_r0[tid] = r0;
+      const uint32_t e = point_list[range.x + base - tid];
+      const uint32_t g = pl_id(e);
+      my_mask = pl_mask(e);
+      s_r0[tid] = rec[3 * (int64_t)g + 0];
       s_r1[tid] = rec[3 * (int64_t)g + 1];
+      const float4 r2 = rec[3 * (int64_t)g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
       my_slot = row_slot(goff[g], rect[g], tile_x, tile_y);
     }
-    // which waves' strips this element can touch; wave w visits only its hits, and the combine below
+    // which waves' quadrants this element can touch; wave w visits only its hits, and the combine below
     // takes zero for the others (exactly what a visit with no valid lane would have produced)
-    const uint32_t my_mask = publish_strip_masks(tid < cnt, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
+    publish_quad_masks(my_mask, s_bits);
     __syncthreads();
     for (int cc = 0; cc < 4; ++cc) {
       uint64_t bits = wave_bits(s_bits, w, cc);

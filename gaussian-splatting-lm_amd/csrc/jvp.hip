@@ -32,7 +32,7 @@ struct JvpPix {
 };
 
 // Front-to-back tangent pass over the tile.  Block-uniform; blockDim = 256.  Wave w visits only the
-// batch elements whose alpha box reaches its 16x4 strip (publish_strip_masks); the stop decision is
+// batch elements whose alpha region reaches its 8x8 quadrant (publish_quad_masks); the stop decision is
 // frozen at the primal (`last` = n_contrib).
 template <bool WITH_XY, bool WITH_INV>
 __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, float pyf, int tile_x, int tile_y,
@@ -52,20 +52,21 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
     const int num_done = block_count(done, s_cnt);
     if (num_done == TILE_PIX) break;
     const int k = r * TILE_PIX + tid;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r0;
+    uint32_t m = 0u;
     if (k < n) {
-      const uint32_t g = point_list[range.x + k];
-      r0 = rec[3 * (int64_t)g + 0];
-      r2 = rec[3 * (int64_t)g + 2];
-      s_r0[tid] = r0;
-      s_r1[tid] = rec[3 * (int64_t)g + 1];
+      const uint32_t e = point_list[range.x + k];
+      const int64_t g = pl_id(e);
+      m = pl_mask(e);
+      s_r0[tid] = rec[3 * g + 0];
+      s_r1[tid] = rec[3 * g + 1];
+      const float4 r2 = rec[3 * g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
-      s_t0[tid] = trec[3 * (int64_t)g + 0];
-      s_t1[tid] = trec[3 * (int64_t)g + 1];
-      const float4 t2 = trec[3 * (int64_t)g + 2];
+      s_t0[tid] = trec[3 * g + 0];
+      s_t1[tid] = trec[3 * g + 1];
+      const float4 t2 = trec[3 * g + 2];
       s_t2[tid] = make_float2(t2.x, t2.y);
     }
-    publish_strip_masks(k < n, r0.x, r0.y, __float_as_uint(r2.w), tile_x, tile_y, s_bits);
+    publish_quad_masks(m, s_bits);
     __syncthreads();
     bool wave_live = __ballot(!done) != 0ull;
     for (int c = 0; c < 4 && wave_live; ++c) {
@@ -121,7 +122,8 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
-  const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
   const bool inside = px < v.W && py < v.H;
   const int64_t pid = (int64_t)py * v.W + px;
   const uint32_t last = inside ? n_contrib[pid] : 0u;
@@ -166,7 +168,8 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
-  const int px = tile_x * TILE_X + (tid & 15), py = tile_y * TILE_Y + (tid >> 4);
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
   const bool inside = px < v.W && py < v.H;
   const int64_t pid = (int64_t)py * v.W + px;
   const int64_t HW = (int64_t)v.H * v.W;

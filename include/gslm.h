@@ -55,7 +55,8 @@ typedef struct gslm_view {
   int32_t sh_degree;    /* active SH degree D */
   int32_t prefiltered;
   int32_t antialiasing;
-  int32_t debug;
+  int32_t debug;        /* nonzero: exhaustive tile traversal -- every wave visits every list entry, as
+                           upstream does (the quadrant cull is off; results are bit-identical either way) */
 } gslm_view;
 
 /* Per-Gaussian inputs.  With raw = 0 they are the activated tensors the rasterizer receives
