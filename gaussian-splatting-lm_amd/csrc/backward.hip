@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
   __shared__ float2 s_r2[TILE_PIX];
   __shared__ uint64_t s_bits[16];
-  __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV>()];
+  __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV, TILE_PIX>()];
   __shared__ int s_misc[4];
   const int tile = blockIdx.x;
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   }
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, d0, d1, d2, di);
-  vjp_tile<WITH_XY, WITH_INV, 3>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
+  vjp_tile<WITH_XY, WITH_INV, 3, TILE_PIX>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
                                  rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows);
 }
 

@@ -54,11 +54,11 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   const uint2 rc = rect[g];
   const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
   const float4 r0 = rec[3 * (int64_t)g + 0];
-  const float C = rec[3 * (int64_t)g + 1].x, tq = rec[3 * (int64_t)g + 2].w;
+  const QuadCull qc = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, rec[3 * (int64_t)g + 1].x, rec[3 * (int64_t)g + 2].w);
   for (int ty = y0; ty < y1; ++ty)
     for (int tx = x0; tx < x1; ++tx) {
       keys[off] = (uint32_t)(ty * gx + tx);
-      vals[off] = g | (quad_mask4(r0.x, r0.y, r0.z, r0.w, C, tq, tx, ty) << ID_BITS);
+      vals[off] = g | (quad_mask(qc, tx, ty) << ID_BITS);
       ++off;
     }
 }
@@ -118,37 +118,39 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
     }
     publish_quad_masks(m, s_bits);
     __syncthreads();
-    // this wave visits, in list order, only the batch elements whose alpha region reaches its quadrant
-    bool wave_live = __ballot(!done) != 0ull;
-    for (int c = 0; c < 4 && wave_live; ++c) {
-      uint64_t bits = wave_bits(s_bits, w, c);
-      while (bits != 0ull && wave_live) {
-        const int j = 64 * c + (int)__builtin_ctzll(bits);
-        bits &= bits - 1ull;
-        if (!done) {
-          const float4 a = s_r0[j];
-          const float4 b = s_r1[j];
-          const float dx = a.x - pxf, dy = a.y - pyf;
-          const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-          const float alpha = fminf(0.99f, b.y * gexp(power));
-          if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) {
-              done = true;
-            } else {
-              const float2 cc = s_r2[j];
-              const float wt = alpha * T;
-              C0 += b.z * wt;
-              C1 += b.w * wt;
-              C2 += cc.x * wt;
-              Dp += cc.y * wt;
-              T = test_T;
-              last = (uint32_t)(k - tid + j + 1);  // 1-based list position
-            }
+    // this wave visits, in list order, only the batch elements whose alpha region reaches its quadrant;
+    // software-pipelined: the next hit's records load while this one computes
+    HitIter it(s_bits, w);
+    int j = __ballot(!done) != 0ull ? it.next() : -1;
+    float4 a = s_r0[max(j, 0)], b = s_r1[max(j, 0)];
+    float2 cc = s_r2[max(j, 0)];
+    while (j >= 0) {
+      const int jn = it.next();
+      const float4 an = s_r0[max(jn, 0)], bn = s_r1[max(jn, 0)];
+      const float2 ccn = s_r2[max(jn, 0)];
+      if (!done) {
+        const float dx = a.x - pxf, dy = a.y - pyf;
+        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float alpha = fminf(0.99f, b.y * gexp(power));
+        if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+          const float test_T = T * (1.0f - alpha);
+          if (test_T < 0.0001f) {
+            done = true;
+          } else {
+            const float wt = alpha * T;
+            C0 += b.z * wt;
+            C1 += b.w * wt;
+            C2 += cc.x * wt;
+            Dp += cc.y * wt;
+            T = test_T;
+            last = (uint32_t)(k - tid + j + 1);  // 1-based list position
           }
         }
-        wave_live = __ballot(!done) != 0ull;
       }
+      j = __ballot(!done) != 0ull ? jn : -1;
+      a = an;
+      b = bn;
+      cc = ccn;
     }
   }
   if (inside) {

@@ -74,47 +74,74 @@ __device__ __forceinline__ float alpha_threshold(float op_eff) {
   return f;
 }
 
-// min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of a x^2 + 2 b x y + c y^2,
-// for a, c > 0 and a c > b^2: 0 if the rectangle holds the centre, else attained on an edge.
-__device__ __forceinline__ double rect_qmin(double a, double b, double c, double x0, double x1, double y0, double y1) {
+// Per-Gaussian part of the quadrant test (k_duplicate prepares it once and tests every tile of the
+// rect).  mode: 0 = reaches no pixel, 1 = treat every quadrant as reachable, 2 = test.
+struct QuadCull {
+  double gx, gy, a, b, c, nba, nbc, tq;
+  int mode;
+};
+
+// NaN-safe: any NaN input yields mode 1 ("reachable").
+__device__ __forceinline__ QuadCull quad_cull_prep(float gx, float gy, float A, float B, float C, float tq) {
+  QuadCull q;
+  q.mode = 2;
+#ifdef GSLM_NO_STRIP_CULL
+  q.mode = 1;
+  return q;
+#endif
+  if (tq < 0.0f) {
+    q.mode = 0;
+    return q;
+  }
+  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
+  q.a = (double)A - e;
+  q.c = (double)C - e;
+  q.b = (double)B;
+  if (!(q.a > 0.0 && q.c > 0.0 && q.a * q.c - q.b * q.b > 0.0)) {  // unbounded (or NaN) region
+    q.mode = 1;
+    return q;
+  }
+  q.nba = -q.b / q.a;  // edge minimisers; their rounding changes the edge minimum only to second order
+  q.nbc = -q.b / q.c;
+  q.gx = (double)gx;
+  q.gy = (double)gy;
+  q.tq = (double)tq;
+  return q;
+}
+
+// min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of a x^2 + 2 b x y + c y^2
+// (positive definite): 0 if the rectangle holds the centre, else attained on an edge.
+__device__ __forceinline__ double rect_qmin(const QuadCull& q, double x0, double x1, double y0, double y1) {
   if (x0 <= 0.0 && x1 >= 0.0 && y0 <= 0.0 && y1 >= 0.0) return 0.0;
   double best = INFINITY;
   const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const double xe = xs[k];
-    const double y = fmin(fmax(-b * xe / c, y0), y1);
-    best = fmin(best, (a * xe + 2.0 * b * y) * xe + c * y * y);
+    const double y = fmin(fmax(q.nbc * xe, y0), y1);
+    best = fmin(best, (q.a * xe + 2.0 * q.b * y) * xe + q.c * y * y);
     const double ye = ys[k];
-    const double x = fmin(fmax(-b * ye / a, x0), x1);
-    best = fmin(best, (c * ye + 2.0 * b * x) * ye + a * x * x);
+    const double x = fmin(fmax(q.nba * ye, x0), x1);
+    best = fmin(best, (q.c * ye + 2.0 * q.b * x) * ye + q.a * x * x);
   }
   return best;
 }
 
 // Quadrant mask of a Gaussian in tile (tile_x, tile_y): bit s set when its alpha region can reach
-// quadrant s = pixels [8 (s & 1), +7] x [8 (s >> 1), +7] of the tile (wave s).  NaN-safe: any NaN
-// input yields "reachable".
-__device__ __forceinline__ uint32_t quad_mask4(float gx, float gy, float A, float B, float C, float tq, int tile_x,
-                                               int tile_y) {
-#ifdef GSLM_NO_STRIP_CULL
-  return 0xFu;
-#endif
-  if (tq < 0.0f) return 0u;
-  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
-  const double a = (double)A - e, c = (double)C - e, b = (double)B;
-  if (!(a > 0.0 && c > 0.0 && a * c - b * b > 0.0)) return 0xFu;  // unbounded (or NaN) region
-  const double bx = (double)(tile_x * TILE_X) - (double)gx, by = (double)(tile_y * TILE_Y) - (double)gy;
+// quadrant s = pixels [8 (s & 1), +7] x [8 (s >> 1), +7] of the tile (wave s).
+__device__ __forceinline__ uint32_t quad_mask(const QuadCull& q, int tile_x, int tile_y) {
+  if (q.mode != 2) return q.mode ? 0xFu : 0u;
+  const double bx = (double)(tile_x * TILE_X) - q.gx, by = (double)(tile_y * TILE_Y) - q.gy;
   uint32_t m = 0u;
-#pragma unroll 1
+#pragma unroll
   for (int s = 0; s < 4; ++s) {
     const double x0 = bx + 8.0 * (s & 1), y0 = by + 8.0 * (s >> 1);
-    if (!(rect_qmin(a, b, c, x0, x0 + 7.0, y0, y0 + 7.0) > (double)tq)) m |= 1u << s;
+    if (!(rect_qmin(q, x0, x0 + 7.0, y0, y0 + 7.0) > q.tq)) m |= 1u << s;
   }
   return m;
 }
 
-// point_list entries carry the Gaussian id in the low 28 bits and its quadrant mask (quad_mask4,
+// point_list entries carry the Gaussian id in the low 28 bits and its quadrant mask (quad_mask,
 // computed once per (tile, Gaussian) pair by k_duplicate) in the top 4 bits.
 constexpr int ID_BITS = 28;
 constexpr uint32_t ID_MASK = (1u << ID_BITS) - 1u;
@@ -149,6 +176,24 @@ __device__ __forceinline__ uint64_t wave_bits(const uint64_t* s_bits, int s, int
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
+
+// Wave-uniform iterator over wave s's hit set of the current batch, in list order.
+struct HitIter {
+  const uint64_t* s_bits;
+  uint64_t cur;
+  int s, c;
+  __device__ __forceinline__ HitIter(const uint64_t* sb, int s_) : s_bits(sb), s(s_), c(0) { cur = wave_bits(sb, s_, 0); }
+  // next batch index, or -1 once the set is exhausted
+  __device__ __forceinline__ int next() {
+    while (cur == 0ull) {
+      if (c == 3) return -1;
+      cur = wave_bits(s_bits, s, ++c);
+    }
+    const int j = 64 * c + (int)__builtin_ctzll(cur);
+    cur &= cur - 1ull;
+    return j;
+  }
+};
 
 // Activated scale / rotation of Gaussian i (fusing exp / normalize when RAW).
 template <bool RAW>

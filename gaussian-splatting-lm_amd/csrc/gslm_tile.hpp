@@ -150,13 +150,16 @@ __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside,
   s.last_inv = 0.f;
 }
 
-// LDS floats needed by vjp_tile's per-wave partial sums
-template <bool WITH_XY, bool WITH_INV>
-constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * TILE_PIX; }
+// LDS floats needed by vjp_tile's per-wave partial sums: [wave][value slot][batch element], rows padded
+// to BATCH + 1 floats so the 8 lanes storing one element's 8 slots hit 8 different banks.
+template <int BATCH>
+constexpr int acc_stride() { return BATCH + 1; }
+template <bool WITH_XY, bool WITH_INV, int BATCH>
+constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * acc_stride<BATCH>(); }
 
 // Back-to-front pass over the tile's list (upstream BACKWARD::renderCUDA semantics), writing one
 // reduced row per (tile, Gaussian) pair.  Block-uniform control flow; requires blockDim = 256.
-template <bool WITH_XY, bool WITH_INV, int ROWF4>
+template <bool WITH_XY, bool WITH_INV, int ROWF4, int BATCH>
 __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint2 range, const uint32_t* __restrict__ point_list,
                                          const float4* __restrict__ rec, const uint2* __restrict__ rect,
@@ -164,6 +167,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
                                          float2* s_r2, uint64_t* s_bits, float* s_acc, int* s_misc,
                                          float4* __restrict__ rows) {
   constexpr int NU = n_used<WITH_XY, WITH_INV>();
+  constexpr int ACC_STRIDE = acc_stride<BATCH>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // Positions >= max over pixels of n_contrib are never blended: their rows are zero.  The leading
   // barrier lets s_misc alias LDS the caller used before this pass (k_render_matvec's JVP buffers).
@@ -181,10 +185,10 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       store_row<ROWF4>(rows, row_slot(goff[g], rect[g], tile_x, tile_y), z);
     }
   }
-  const int rounds = (n_eff + TILE_PIX - 1) / TILE_PIX;
+  const int rounds = (n_eff + BATCH - 1) / BATCH;
   for (int r = 0; r < rounds; ++r) {
-    const int base = n_eff - 1 - r * TILE_PIX;  // list position of batch element 0
-    const int cnt = min(TILE_PIX, base + 1);
+    const int base = n_eff - 1 - r * BATCH;  // list position of batch element 0
+    const int cnt = min(BATCH, base + 1);
     __syncthreads();
     uint32_t my_slot = 0;
     uint32_t my_mask = 0u;
@@ -202,15 +206,12 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     // takes zero for the others (exactly what a visit with no valid lane would have produced)
     publish_quad_masks(my_mask, s_bits);
     __syncthreads();
-    for (int cc = 0; cc < 4; ++cc) {
-      uint64_t bits = wave_bits(s_bits, w, cc);
-      while (bits != 0ull) {
-        const int j = 64 * cc + (int)__builtin_ctzll(bits);
-        bits &= bits - 1ull;
+    HitIter it(s_bits, w);
+    for (int j = it.next(); j >= 0; j = it.next()) {
+      const float4 a = s_r0[j], b = s_r1[j];
+      const float2 c = s_r2[j];
+      {
         const uint32_t contributor = (uint32_t)(base - j);  // 0-based list position
-        const float4 a = s_r0[j];
-        const float4 b = s_r1[j];
-        const float2 c = s_r2[j];
         const float dx = a.x - pxf, dy = a.y - pyf;
         const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
         const float G = gexp(power);
@@ -267,7 +268,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
             rr = wave_reduce8_t(pv, lane);
           }
           const int k = lane >> 3;
-          if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * TILE_PIX + j] = rr;
+          if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * ACC_STRIDE + j] = rr;
         } else {
           if (any) {
 #pragma unroll
@@ -278,7 +279,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
 #pragma unroll
             for (int q = 0; q < NV; ++q)
               if (q_used<WITH_XY, WITH_INV>(q))
-                s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * TILE_PIX + j] = any ? gv[q] : 0.f;
+                s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * ACC_STRIDE + j] = any ? gv[q] : 0.f;
           }
         }
       }
@@ -291,10 +292,10 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         t[q] = 0.f;
         if (q_used<WITH_XY, WITH_INV>(q)) {
           const int sq = q_slot<WITH_XY, WITH_INV>(q);
-          const float p0 = (my_mask & 1u) ? s_acc[(0 * NU + sq) * TILE_PIX + tid] : 0.f;
-          const float p1 = (my_mask & 2u) ? s_acc[(1 * NU + sq) * TILE_PIX + tid] : 0.f;
-          const float p2 = (my_mask & 4u) ? s_acc[(2 * NU + sq) * TILE_PIX + tid] : 0.f;
-          const float p3 = (my_mask & 8u) ? s_acc[(3 * NU + sq) * TILE_PIX + tid] : 0.f;
+          const float p0 = (my_mask & 1u) ? s_acc[(0 * NU + sq) * ACC_STRIDE + tid] : 0.f;
+          const float p1 = (my_mask & 2u) ? s_acc[(1 * NU + sq) * ACC_STRIDE + tid] : 0.f;
+          const float p2 = (my_mask & 4u) ? s_acc[(2 * NU + sq) * ACC_STRIDE + tid] : 0.f;
+          const float p3 = (my_mask & 8u) ? s_acc[(3 * NU + sq) * ACC_STRIDE + tid] : 0.f;
           t[q] = ((p0 + p1) + p2) + p3;
         }
       }

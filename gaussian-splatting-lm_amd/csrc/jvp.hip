@@ -12,6 +12,8 @@
 
 namespace gslm {
 
+constexpr int MATVEC_BATCH = 128;
+
 template <bool RAW>
 __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
                                                          const float4* __restrict__ rec,
@@ -31,10 +33,11 @@ struct JvpPix {
   float T, dT, dC[3], dD;
 };
 
-// Front-to-back tangent pass over the tile.  Block-uniform; blockDim = 256.  Wave w visits only the
+// Front-to-back tangent pass over the tile, BATCH list entries staged in LDS per round.
+// Block-uniform; blockDim = 256.  Wave w visits only the
 // batch elements whose alpha region reaches its 8x8 quadrant (publish_quad_masks); the stop decision is
 // frozen at the primal (`last` = n_contrib).
-template <bool WITH_XY, bool WITH_INV>
+template <bool WITH_XY, bool WITH_INV, int BATCH>
 __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint32_t last, uint2 range, const uint32_t* __restrict__ point_list,
                                          const float4* __restrict__ rec, const float4* __restrict__ trec,
@@ -47,13 +50,13 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
   o.dD = 0.f;
   bool done = !inside || last == 0;
   const int n = (int)(range.y - range.x);
-  const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
+  const int rounds = (n + BATCH - 1) / BATCH;
   for (int r = 0; r < rounds; ++r) {
     const int num_done = block_count(done, s_cnt);
     if (num_done == TILE_PIX) break;
-    const int k = r * TILE_PIX + tid;
+    const int k = r * BATCH + tid;
     uint32_t m = 0u;
-    if (k < n) {
+    if (tid < BATCH && k < n) {
       const uint32_t e = point_list[range.x + k];
       const int64_t g = pl_id(e);
       m = pl_mask(e);
@@ -68,42 +71,33 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
     }
     publish_quad_masks(m, s_bits);
     __syncthreads();
-    bool wave_live = __ballot(!done) != 0ull;
-    for (int c = 0; c < 4 && wave_live; ++c) {
-      uint64_t bits = wave_bits(s_bits, w, c);
-      while (bits != 0ull && wave_live) {
-        const int j = 64 * c + (int)__builtin_ctzll(bits);
-        bits &= bits - 1ull;
-        if (!done) {
-          const float4 a = s_r0[j];
-          const float4 b = s_r1[j];
-          const float dx = a.x - pxf, dy = a.y - pyf;
-          const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-          const float G = gexp(power);
-          const float alpha = fminf(0.99f, b.y * G);
-          if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-            const float2 cc = s_r2[j];
-            const float4 t0 = s_t0[j];
-            const float4 t1 = s_t1[j];
-            const float2 t2 = s_t2[j];
-            float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
-            if (WITH_XY) {
-              const float ddx = t0.x, ddy = t0.y;
-              dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
-            }
-            const float dalpha = G * (t1.y + b.y * dpower);
-            const float wt = alpha * o.T;
-            const float dw = dalpha * o.T + alpha * o.dT;
-            o.dC[0] += t1.z * wt + b.z * dw;
-            o.dC[1] += t1.w * wt + b.w * dw;
-            o.dC[2] += t2.x * wt + cc.x * dw;
-            if (WITH_INV) o.dD += t2.y * wt + cc.y * dw;
-            o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
-            o.T = o.T * (1.f - alpha);
-            if ((uint32_t)(k - tid + j + 1) == last) done = true;
+    // software-pipelined over this wave's hits: the next hit's records load while this one computes
+    HitIter it(s_bits, w);
+    for (int j = __ballot(!done) != 0ull ? it.next() : -1; j >= 0; j = __ballot(!done) != 0ull ? it.next() : -1) {
+      const float4 a = s_r0[j], b = s_r1[j], t0 = s_t0[j], t1 = s_t1[j];
+      const float2 cc = s_r2[j], t2 = s_t2[j];
+      if (!done) {
+        const float dx = a.x - pxf, dy = a.y - pyf;
+        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float G = gexp(power);
+        const float alpha = fminf(0.99f, b.y * G);
+        if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+          float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
+          if (WITH_XY) {
+            const float ddx = t0.x, ddy = t0.y;
+            dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
           }
+          const float dalpha = G * (t1.y + b.y * dpower);
+          const float wt = alpha * o.T;
+          const float dw = dalpha * o.T + alpha * o.dT;
+          o.dC[0] += t1.z * wt + b.z * dw;
+          o.dC[1] += t1.w * wt + b.w * dw;
+          o.dC[2] += t2.x * wt + cc.x * dw;
+          if (WITH_INV) o.dD += t2.y * wt + cc.y * dw;
+          o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
+          o.T = o.T * (1.f - alpha);
+          if ((uint32_t)(k - tid + j + 1) == last) done = true;
         }
-        wave_live = __ballot(!done) != 0ull;
       }
     }
   }
@@ -115,8 +109,9 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
                                                      const float4* __restrict__ rec, const float4* __restrict__ trec,
                                                      const uint32_t* __restrict__ n_contrib,
                                                      float* __restrict__ out_color_t, float* __restrict__ out_inv_t) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX], s_t0[TILE_PIX], s_t1[TILE_PIX];
-  __shared__ float2 s_r2[TILE_PIX], s_t2[TILE_PIX];
+  constexpr int B = TILE_PIX;
+  __shared__ float4 s_r0[B], s_r1[B], s_t0[B], s_t1[B];
+  __shared__ float2 s_r2[B], s_t2[B];
   __shared__ uint64_t s_bits[16];
   __shared__ int s_cnt[4];
   const int tile = blockIdx.x;
@@ -128,7 +123,7 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   const int64_t pid = (int64_t)py * v.W + px;
   const uint32_t last = inside ? n_contrib[pid] : 0u;
   JvpPix o;
-  jvp_tile<WITH_XY, true>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec, trec,
+  jvp_tile<WITH_XY, true, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec, trec,
                           s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   if (inside) {
     const int64_t HW = (int64_t)v.H * v.W;
@@ -149,20 +144,22 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
                                                         const float* __restrict__ final_T,
                                                         const uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ weight, float4* __restrict__ contrib) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
-  __shared__ float2 s_r2[TILE_PIX];
+  // 128-entry batches: 19.7 KB of LDS per block -> 8 blocks (VGPR-limited to 6 waves per SIMD) per CU,
+  // the occupancy this latency-bound pass needs
+  constexpr int B = MATVEC_BATCH;
+  __shared__ float4 s_r0[B], s_r1[B];
+  __shared__ float2 s_r2[B];
   __shared__ uint64_t s_bits[16];
   __shared__ int s_cnt[4];
   // The JVP pass's tangent records and the VJP pass's per-wave partials (+ its n_eff scratch) are
   // never live together (vjp_tile starts with a block barrier): one LDS region.
-  // LM path: 10 KB + 28 KB (+ 10 KB records, masks) = 38.1 KB per block -> 4 blocks per CU.
-  constexpr int kAcc = vjp_acc_floats<WITH_XY, false>();
-  constexpr int kTan = (4 + 4 + 2) * TILE_PIX;
-  static_assert(kAcc >= kTan, "tangent records fit in the partial-sum region");
-  __shared__ float4 s_union[kAcc / 4];
+  constexpr int kAcc = vjp_acc_floats<WITH_XY, false, B>();
+  constexpr int kTan = (4 + 4 + 2) * B;
+  constexpr int kU = ((kAcc > kTan ? kAcc : kTan) + 3) / 4;
+  __shared__ float4 s_union[kU];
   float4* s_t0 = s_union;
-  float4* s_t1 = s_union + TILE_PIX;
-  float2* s_t2 = reinterpret_cast<float2*>(s_union + 2 * TILE_PIX);
+  float4* s_t1 = s_union + B;
+  float2* s_t2 = reinterpret_cast<float2*>(s_union + 2 * B);
   float* s_acc = reinterpret_cast<float*>(s_union);
   int* s_misc = reinterpret_cast<int*>(s_union);
   const int tile = blockIdx.x;
@@ -184,7 +181,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
     w2 = weight[2 * HW + pid];
   }
   JvpPix o;
-  jvp_tile<WITH_XY, false>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
+  jvp_tile<WITH_XY, false, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
                            s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   // u = 2 * w (.) (J v)   -- factor 2: the [r; r] residual aliasing of batch_training_loss.py:17
   const float u0 = 2.f * w0 * (o.dC[0] + o.dT * v.bg[0]);
@@ -192,7 +189,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   const float u2 = 2.f * w2 * (o.dC[2] + o.dT * v.bg[2]);
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
-  vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
+  vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
                                             rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib);
 }
 
