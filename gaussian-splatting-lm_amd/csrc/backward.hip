@@ -93,18 +93,57 @@ struct FlatK {
   double* dot_part;   // per-block partials of <v, y> over the written elements (NULL = off)
 };
 
-// y[idx] (op)= val (+ d v[idx]); returns v[idx] * y_new for the fused <v, y> (0 when dot is off)
-__device__ __forceinline__ double emit(float* y, const float* v, float d, int use_damp, int overwrite, bool dot,
-                                       int64_t idx, float val) {
-  const float vv = (use_damp || dot) ? v[idx] : 0.f;
-  if (use_damp) val += d * vv;
-  float out = val;
-  if (overwrite) y[idx] = val;
-  else {
-    out = y[idx] + val;
-    y[idx] = out;
+// Block-cooperative version of sum_rows for the 256 consecutive Gaussians of a block: their rows are
+// one contiguous range (row_slot groups rows by Gaussian index), streamed through LDS in chunks of
+// GATHER_CHUNK rows with coalesced float4 loads; each thread then adds its own rows from LDS, in the
+// same order as sum_rows (bitwise-identical sums).  Must be called by all 256 threads.
+constexpr int GATHER_CHUNK = 512;
+template <int ROWF4>
+__device__ __forceinline__ void block_sum_rows(const float4* __restrict__ rows, uint32_t R0, uint32_t R1,
+                                               uint32_t my_off, uint32_t my_n, float4* s_buf, float G2[NV]) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q) G2[q] = 0.f;
+  const uint32_t my_end = my_off + my_n;
+  for (uint32_t c0 = R0; c0 < R1; c0 += GATHER_CHUNK) {
+    const uint32_t cn = min((uint32_t)GATHER_CHUNK, R1 - c0);
+    __syncthreads();  // the previous chunk has been consumed
+    for (uint32_t e = threadIdx.x; e < cn * ROWF4; e += blockDim.x) s_buf[e] = rows[(size_t)c0 * ROWF4 + e];
+    __syncthreads();
+    const uint32_t lo = max(my_off, c0), hi = min(my_end, c0 + cn);
+    for (uint32_t r = lo; r < hi; ++r) {
+      float t[NV];
+      load_row<ROWF4>(s_buf, r - c0, t);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) G2[q] += t[q];
+    }
   }
-  return dot ? (double)vv * (double)out : 0.0;
+  __syncthreads();  // s_buf may be reused by the caller
+}
+
+template <int K>
+__device__ __forceinline__ void load_group(const float* v, const float* y, int64_t base, bool need_v, bool need_y,
+                                           float vin[K], float yold[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    vin[k] = need_v ? v[base + k] : 0.f;
+    yold[k] = need_y ? y[base + k] : 0.f;
+  }
+}
+
+// y = (overwrite ? 0 : y_old) + val + d v; returns sum of v * y_new (0 when dot is off)
+template <int K>
+__device__ __forceinline__ double store_group(float* y, float d, int use_damp, int64_t base, int overwrite, bool dot,
+                                              const float val[K], const float vin[K], const float yold[K]) {
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float x = val[k];
+    if (use_damp) x += d * vin[k];
+    const float out = overwrite ? x : yold[k] + x;
+    y[base + k] = out;
+    if (dot) acc += (double)vin[k] * (double)out;
+  }
+  return acc;
 }
 
 template <bool WANT_MEANS, int ROWF4>
@@ -112,7 +151,7 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
                                                     const float4* __restrict__ rows, FlatK o) {
-  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(K-1)]
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(K-1)], first the row chunks
   __shared__ double s_dot[4];
   const int tid = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
@@ -121,27 +160,39 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
   const int nc = (v.D + 1) * (v.D + 1);
   const bool dot = o.dot_part != nullptr;
   double dacc = 0.0;
+  const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
+  const uint32_t n = i < g.P ? tiles[i] : 0u;
+  float G2[NV];
+  {
+    const int64_t il = i0 + nvalid - 1;
+    const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
+    block_sum_rows<ROWF4>(rows, R0, R1, i < g.P ? goff[i] : R1, n, reinterpret_cast<float4*>(s_rest), G2);
+  }
+  const int u = o.use_damp, ow = o.overwrite;
+  const bool need_v = u || dot;
   if (i < g.P) {
-    const uint32_t n = tiles[i];
-    float G2[NV];
-    sum_rows<ROWF4>(rows, n ? goff[i] : 0u, n, G2);
     ChainOut co;
     chain_vjp<true>(v, g, i, n != 0, rec, G2, WANT_MEANS, co);
-    const int u = o.use_damp, ow = o.overwrite;
+    // Load phase first, store phase second: y may alias nothing, but the compiler cannot know, so
+    // interleaved load/store pairs would serialise on memory latency.
+    const bool xyz_on = WANT_MEANS || ow;
+    float vx[3], yx[3], vdc[3], ydc[3], vs[3], ys[3], vr[4], yr[4], vo[1], yo[1];
+    load_group<3>(o.v[0], o.y[0], 3 * i, xyz_on && need_v, xyz_on && !ow, vx, yx);
+    load_group<3>(o.v[1], o.y[1], 3 * i, need_v, !ow, vdc, ydc);
+    load_group<3>(o.v[3], o.y[3], 3 * i, need_v, !ow, vs, ys);
+    load_group<4>(o.v[4], o.y[4], 4 * i, need_v, !ow, vr, yr);
+    load_group<1>(o.v[5], o.y[5], i, need_v, !ow, vo, yo);
     if (WANT_MEANS) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dacc += emit(o.y[0], o.v[0], o.damp[0], u, ow, dot, 3 * i + k, co.dmean[k]);
+      dacc += store_group<3>(o.y[0], o.damp[0], u, 3 * i, ow, dot, co.dmean, vx, yx);
     } else if (ow) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dacc += emit(o.y[0], o.v[0], o.damp[0], u, 1, dot && u, 3 * i + k, 0.f);
+      const float z[3] = {0.f, 0.f, 0.f};
+      dacc += store_group<3>(o.y[0], o.damp[0], u, 3 * i, 1, dot && u, z, vx, yx);
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) dacc += emit(o.y[1], o.v[1], o.damp[1], u, ow, dot, 3 * i + k, co.dsh[0][k]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) dacc += emit(o.y[3], o.v[3], o.damp[3], u, ow, dot, 3 * i + k, co.dscale[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dacc += emit(o.y[4], o.v[4], o.damp[4], u, ow, dot, 4 * i + k, co.drot[k]);
-    dacc += emit(o.y[5], o.v[5], o.damp[5], u, ow, dot, i, co.dop);
+    dacc += store_group<3>(o.y[1], o.damp[1], u, 3 * i, ow, dot, co.dsh[0], vdc, ydc);
+    dacc += store_group<3>(o.y[3], o.damp[3], u, 3 * i, ow, dot, co.dscale, vs, ys);
+    dacc += store_group<4>(o.y[4], o.damp[4], u, 4 * i, ow, dot, co.drot, vr, yr);
+    const float dop[1] = {co.dop};
+    dacc += store_group<1>(o.y[5], o.damp[5], u, i, ow, dot, dop, vo, yo);
 #pragma unroll
     for (int k = 1; k < 16; ++k)
       if (k < g.M) {
@@ -150,11 +201,31 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
       }
   }
   __syncthreads();
-  // coalesced store of the block's contiguous [nvalid * R] slice of the SH-rest group
-  const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
-  const int64_t base = i0 * R;
-  for (int64_t e = tid; e < nvalid * R; e += blockDim.x)
-    dacc += emit(o.y[2], o.v[2], o.damp[2], o.use_damp, o.overwrite, dot, base + e, s_rest[e]);
+  // coalesced store of the block's contiguous [nvalid * R] slice of the SH-rest group, 8 elements per
+  // thread per step with all loads issued before any store
+  const int64_t base = i0 * R, total = nvalid * R;
+  constexpr int U = 8;
+  for (int64_t e0 = 0; e0 < total; e0 += (int64_t)U * blockDim.x) {
+    float vin[U], yold[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t e = e0 + (int64_t)k * blockDim.x + tid;
+      const bool in = e < total;
+      vin[k] = (in && need_v) ? o.v[2][base + e] : 0.f;
+      yold[k] = (in && !ow) ? o.y[2][base + e] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t e = e0 + (int64_t)k * blockDim.x + tid;
+      if (e < total) {
+        float val = s_rest[e];
+        if (u) val += o.damp[2] * vin[k];
+        const float out = ow ? val : yold[k] + val;
+        o.y[2][base + e] = out;
+        if (dot) dacc += (double)vin[k] * (double)out;
+      }
+    }
+  }
   if (dot) {
     const int lane = tid & 63, w = tid >> 6;
 #pragma unroll
@@ -215,7 +286,9 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
     for (int k = 0; k < 6; ++k)
       if (!o.v[k] && !(k == 2 && g.M == 1)) { set_error("damping needs every group of v"); return GSLM_ERR_INVALID; }
   const unsigned nb = (unsigned)((g.P + 255) / 256);
-  const size_t lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float) + 16;
+  const size_t rest_lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float);
+  const size_t chunk_lds = (size_t)GATHER_CHUNK * (mask_xyz ? 2 : 3) * sizeof(float4);
+  const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
   if (mask_xyz)
     hipLaunchKernelGGL((k_gather_lm<false, 2>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
                        sb.contrib, o);

@@ -71,7 +71,8 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
     }
     publish_quad_masks(m, s_bits);
     __syncthreads();
-    // software-pipelined over this wave's hits: the next hit's records load while this one computes
+    // this wave's hits in list order, while any of its pixels is still live (latency is hidden by
+    // occupancy -- 8 waves per SIMD -- rather than by register prefetch, which costs the occupancy)
     HitIter it(s_bits, w);
     for (int j = __ballot(!done) != 0ull ? it.next() : -1; j >= 0; j = __ballot(!done) != 0ull ? it.next() : -1) {
       const float4 a = s_r0[j], b = s_r1[j], t0 = s_t0[j], t1 = s_t1[j];
@@ -181,16 +182,24 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
     w2 = weight[2 * HW + pid];
   }
   JvpPix o;
+#ifdef GSLM_EXPERIMENT_SKIP_JVP
+  o.dC[0] = o.dC[1] = o.dC[2] = o.dT = 1e-3f;
+#else
   jvp_tile<WITH_XY, false, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
                            s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
+#endif
   // u = 2 * w (.) (J v)   -- factor 2: the [r; r] residual aliasing of batch_training_loss.py:17
   const float u0 = 2.f * w0 * (o.dC[0] + o.dT * v.bg[0]);
   const float u1 = 2.f * w1 * (o.dC[1] + o.dT * v.bg[1]);
   const float u2 = 2.f * w2 * (o.dC[2] + o.dT * v.bg[2]);
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
+#ifdef GSLM_EXPERIMENT_SKIP_VJP
+  if (u0 + u1 + u2 == 12345.f) contrib[0] = make_float4(u0, u1, u2, 0.f);
+#else
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
                                             rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib);
+#endif
 }
 
 // ------------------------------------------------------------------ launchers
