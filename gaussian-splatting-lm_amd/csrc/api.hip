@@ -337,7 +337,41 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
-  if ((stages & GSLM_STAGE_TANGENT) && (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, s))) return st;
+  XpbyK xp{};
+  const bool fused_xpby = opts && opts->xpby_s;
+  if (fused_xpby) {
+    const gslm_grads* sv = opts->xpby_s;
+    if (!(stages & GSLM_STAGE_TANGENT) || !opts->beta_num || !opts->beta_den) {
+      set_error("matvec: xpby needs the TANGENT stage and beta_num / beta_den");
+      return GSLM_ERR_INVALID;
+    }
+    const int R = 3 * (b.g.M - 1);
+    if (vin->sh_dc_stride != 3 || sv->sh_dc_stride != 3 || (b.g.M > 1 && (vin->sh_rest_stride != R || sv->sh_rest_stride != R))) {
+      set_error("matvec: xpby needs contiguous SH groups (dc stride 3, rest stride 3(M-1))");
+      return GSLM_ERR_INVALID;
+    }
+    float* pp[6] = {vin->means3D, vin->sh_dc, vin->sh_rest, vin->scales, vin->rotations, vin->opacities};
+    const float* ss[6] = {sv->means3D, sv->sh_dc, sv->sh_rest, sv->scales, sv->rotations, sv->opacities};
+    const int ww[6] = {3, 3, R, 3, 4, 1};
+    for (int k = 0; k < 6; ++k) {
+      if ((pp[k] == nullptr) != (ss[k] == nullptr) || (ww[k] == 0 && pp[k])) {
+        set_error("matvec: xpby groups of v and s must match");
+        return GSLM_ERR_INVALID;
+      }
+      xp.p[k] = ww[k] ? pp[k] : nullptr;
+      xp.s[k] = ss[k];
+      xp.w[k] = ww[k];
+    }
+    xp.num = opts->beta_num;
+    xp.den = opts->beta_den;
+    xp.tail_p = opts->xpby_tail_n > 0 ? opts->xpby_tail_v : nullptr;
+    xp.tail_s = opts->xpby_tail_s;
+    xp.tail_n = opts->xpby_tail_n;
+    if (xp.tail_p && !xp.tail_s) { set_error("matvec: xpby tail without s"); return GSLM_ERR_INVALID; }
+  }
+  if ((stages & GSLM_STAGE_TANGENT) &&
+      (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s)))
+    return st;
   if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
       (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
     return st;

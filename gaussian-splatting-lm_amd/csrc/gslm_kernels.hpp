@@ -347,8 +347,21 @@ int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
                       const float* dL_dcolor, const float* dL_dinv, const ScratchBufs& sb, hipStream_t s);
 int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, const BinBufs& bb,
                           const ScratchBufs& sb, const GradK& out, bool want_means, hipStream_t s);
+// Fused CG direction update run by the tangent kernel before it reads the direction: every
+// per-Gaussian group k (xyz, dc, rest, scaling, rotation, opacity) of p becomes s + beta p over its
+// contiguous slice of width w[k] floats per Gaussian, plus a flat tail (the exposure group).
+struct XpbyK {
+  float* p[6];
+  const float* s[6];
+  int w[6];
+  const double* num;
+  const double* den;
+  float* tail_p;
+  const float* tail_s;
+  int64_t tail_n;
+};
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
-                       const ScratchBufs& sb, hipStream_t s);
+                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s);
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);

@@ -14,12 +14,49 @@ namespace gslm {
 
 constexpr int MATVEC_BATCH = 128;
 
-template <bool RAW>
+// p = s + beta p over this block's 256 Gaussians' slices of every group (coalesced, 8 loads in flight
+// per thread), and the flat tail by block 0.  Same arithmetic as k_xpby_dev (bitwise).
+__device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P) {
+  const float b = (float)((*xp.num) / (*xp.den));
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t nv = min((int64_t)blockDim.x, P - i0);
+  constexpr int U = 8;
+  for (int k = 0; k < 6; ++k) {
+    if (!xp.p[k]) continue;
+    float* p = xp.p[k] + i0 * xp.w[k];
+    const float* s = xp.s[k] + i0 * xp.w[k];
+    const int64_t len = nv * xp.w[k];
+    for (int64_t e0 = 0; e0 < len; e0 += (int64_t)U * blockDim.x) {
+      float sv[U], pv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
+        sv[u] = e < len ? s[e] : 0.f;
+        pv[u] = e < len ? p[e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
+        if (e < len) p[e] = sv[u] + b * pv[u];
+      }
+    }
+  }
+  if (blockIdx.x == 0 && xp.tail_p)
+    for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) xp.tail_p[e] = xp.tail_s[e] + b * xp.tail_p[e];
+}
+
+template <bool RAW, bool XPBY>
 __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
                                                          const float4* __restrict__ rec,
                                                          const uint32_t* __restrict__ tiles,
-                                                         float4* __restrict__ trec) {
+                                                         float4* __restrict__ trec, XpbyK xp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (XPBY) {
+    // the direction this kernel reads is the updated one: each thread reads back only its own
+    // Gaussian's elements, all written by this block before the barrier
+    block_xpby(xp, g.P);
+    __syncthreads();
+  }
   if (i >= g.P) return;
   if (tiles[i] == 0) return;  // never gathered by the render passes
   float T2[10];
@@ -204,13 +241,32 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
 
 // ------------------------------------------------------------------ launchers
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
-                       const ScratchBufs& sb, hipStream_t s) {
-  if (g.P == 0) return GSLM_OK;
+                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s) {
+  if (g.P == 0) {
+    if (xp && xp->tail_p) {
+      set_error("internal: fused xpby with P = 0");
+      return GSLM_ERR_INVALID;
+    }
+    return GSLM_OK;
+  }
   const unsigned nb = (unsigned)((g.P + 255) / 256);
-  if (g.raw)
-    hipLaunchKernelGGL(k_preprocess_jvp<true>, dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles, sb.trec);
-  else
-    hipLaunchKernelGGL(k_preprocess_jvp<false>, dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles, sb.trec);
+  XpbyK none{};
+  const XpbyK& x = xp ? *xp : none;
+  if (xp) {
+    if (g.raw)
+      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+                         sb.trec, x);
+    else
+      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+                         sb.trec, x);
+  } else {
+    if (g.raw)
+      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+                         sb.trec, x);
+    else
+      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+                         sb.trec, x);
+  }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -218,7 +274,7 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s) {
-  int st = launch_tangent_pre(v, g, t, m2t, gb, sb, s);
+  int st = launch_tangent_pre(v, g, t, m2t, gb, sb, nullptr, s);
   if (st) return st;
   const int ntiles = v.gx * v.gy;
   const bool xy = t.means3D != nullptr || m2t != nullptr;

@@ -55,6 +55,8 @@ class GslmMatvecOpts(ctypes.Structure):
         ("stages", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("damp7", ctypes.POINTER(ctypes.c_double)), ("dot_vy", ctypes.c_void_p),
         ("dot_scratch", ctypes.c_void_p), ("dot_scratch_bytes", ctypes.c_size_t),
+        ("xpby_s", ctypes.c_void_p), ("beta_num", ctypes.c_void_p), ("beta_den", ctypes.c_void_p),
+        ("xpby_tail_v", ctypes.c_void_p), ("xpby_tail_s", ctypes.c_void_p), ("xpby_tail_n", ctypes.c_int64),
     ]
 
 
@@ -118,6 +120,9 @@ EXPORTS = {
 }
 
 
+ABI_VERSION = 2  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+
+
 class GslmError(RuntimeError):
     pass
 
@@ -131,6 +136,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
+    if lib.gslm_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has C ABI version {lib.gslm_abi_version()}, these bindings need "
+                          f"{ABI_VERSION}: rebuild it")
     return lib
 
 

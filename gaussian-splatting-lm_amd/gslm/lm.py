@@ -139,28 +139,44 @@ class LMProblem:
         self.matvec_dot(v, y, None)
         return y
 
-    def matvec_dot(self, v, y, dot_out):
+    def matvec_dot(self, v, y, dot_out, pre=None):
         """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
-        view; exposure components of v zero, as in every LM iterate).  Returns True if fused."""
+        view; exposure components of v zero, as in every LM iterate).  Returns True if fused.
+        pre = (s, beta_num_ptr, beta_den_ptr): first v <- s + beta v (the deferred CG direction
+        update), fused into the first view's tangent kernel."""
         fuse = dot_out is not None and len(self.views) == 1
-        self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None)
+        self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None, pre=pre)
         return fuse
 
-    def local_normal_matvec(self, v, y, damp=False, dot_out=None):
-        """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y)."""
+    def local_normal_matvec(self, v, y, damp=False, dot_out=None, pre=None):
+        """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y).
+        pre: see matvec_dot."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
         ys = self.layout.grads_struct(y)
+        if pre is not None and not self.views:
+            s, num, den = pre
+            check(lib.gslm_xpby_dev(v.numel(), s.data_ptr(), num, den, v.data_ptr(), self.stream), "gslm_xpby_dev")
+            pre = None
         if not self.views:
             y.zero_()
             if damp:
                 self.damp_add(v, y)
             return y
         last = len(self.views) - 1
+        e0, e1 = self.layout.offsets["exposure"]
         for b, vr in enumerate(self.views):
             opts = _lib.GslmMatvecOpts()
             opts.stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
             opts.damp7 = self._damps if (damp and b == 0) else None
+            if pre is not None and b == 0:
+                s, num, den = pre
+                ss = self.layout.grads_struct(s)
+                opts.xpby_s = ctypes.addressof(ss)
+                opts.beta_num, opts.beta_den = num, den
+                opts.xpby_tail_v = v.data_ptr() + 4 * e0
+                opts.xpby_tail_s = s.data_ptr() + 4 * e0
+                opts.xpby_tail_n = e1 - e0
             if dot_out is not None and b == last:
                 opts.dot_vy = dot_out
                 opts.dot_scratch = self.dot_scratch.data_ptr()
@@ -170,7 +186,6 @@ class LMProblem:
                                           vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
                                           vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts), self.stream),
                   "gslm_matvec_view_ex")
-        e0, e1 = self.layout.offsets["exposure"]
         if damp:
             torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
         else:
@@ -223,9 +238,11 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
         p.copy_(s)
         prob.dot(s, s, ptr(GAM))
         stop = False
+        pre = None
         for _ in range(restart_iter):
+            # [p = s + beta p, deferred from the previous iteration into this product's tangent kernel]
             # q = A p and delta = <p, A p> (= |J p|^2 + p.D.p), fused into the gather when possible
-            if not prob.matvec_dot(p, q, ptr(DEL)):
+            if not prob.matvec_dot(p, q, ptr(DEL), pre=pre):
                 prob.dot(p, q, ptr(DEL))
             if check_every and sc[DEL].item() < 1e-20:
                 if verbose:
@@ -235,7 +252,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             # x += alpha p ; s -= alpha q ; gamma' = <s, s>   (one pass)
             check(lib.gslm_cg_update(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(), s.data_ptr(),
                                      prob.dot_scratch.data_ptr(), ptr(GAMN), st))
-            check(lib.gslm_xpby_dev(n, s.data_ptr(), ptr(GAMN), ptr(GAM), p.data_ptr(), st))
+            # beta = gamma' / gamma; after the slot swap below these are the GAM / GAMN slots
+            pre = (s, ptr(GAMN), ptr(GAM))
             if check_every:
                 prob.dot(x, g, ptr(XG))
                 prob.dot(x, s, ptr(XS))

@@ -57,10 +57,12 @@ class ShardedOperator:
         self.local.rhs(out)
         return self._allreduce(out)
 
-    def matvec_dot(self, v, y, dot_out):
+    def matvec_dot(self, v, y, dot_out, pre=None):
+        kw = {} if pre is None else {"pre": pre}
         if self.world_size == 1:
-            return self.local.matvec_dot(v, y, dot_out)
-        self.local.local_normal_matvec(v, y, damp=False)
+            return self.local.matvec_dot(v, y, dot_out, **kw)
+        # every rank holds the same s, p and scalars, so the deferred p update stays rank-local
+        self.local.local_normal_matvec(v, y, damp=False, **kw)
         self._allreduce(y)
         self.local.damp_add(v, y)
         return False

@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 1
+#define GSLM_ABI_VERSION 2
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -163,6 +163,18 @@ typedef struct gslm_matvec_opts {
   double* dot_vy;         /* device double or NULL: receives <v, y> over the gathered groups after GATHER */
   void* dot_scratch;      /* device scratch for dot_vy, >= gslm_dot_scratch_bytes(P) bytes */
   size_t dot_scratch_bytes;
+  /* Fused CG direction update (the p = s + beta p of conjugate_gradient.py:121-123, deferred into the
+   * next product): when xpby_s is set, before the TANGENT stage every group of v becomes
+   * s + beta v, beta = *beta_num / *beta_den (device doubles), and so does the flat tail
+   * xpby_tail_v[0..xpby_tail_n) (the exposure group) from xpby_tail_s.  v's groups must be
+   * contiguous per Gaussian (sh_dc_stride 3, sh_rest_stride 3(M-1)) and writable.  Same arithmetic
+   * as gslm_xpby_dev. */
+  const gslm_grads* xpby_s;
+  const double* beta_num;
+  const double* beta_den;
+  float* xpby_tail_v;
+  const float* xpby_tail_s;
+  int64_t xpby_tail_n;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,

@@ -121,3 +121,31 @@ def test_lm_step_decreases_loss():
     d, m, cams = _load()
     out = lm_step(m, cams, cams, torch.zeros(3), max_iter=2, restart_iter=1)
     assert out["final_val_loss"] <= out["start_loss"]
+
+
+def test_fused_xpby_matches_separate():
+    """The deferred CG direction update p = s + beta p fused into the tangent kernel (all groups and
+    the exposure tail) gives the same p and the same (J^T J + D) p, bitwise, as gslm_xpby_dev + matvec."""
+    from gslm import _lib
+    from gslm.lm import LMProblem
+    d, m, cams = _load()
+    prob = LMProblem(m, cams[:1], torch.zeros(3))
+    prob.evaluate()
+    n = prob.layout.numel
+    g = torch.Generator().manual_seed(8)
+    s = torch.randn(n, generator=g).cuda()
+    p = torch.randn(n, generator=g).cuda()
+    lo, hi = prob.layout.offsets["xyz"]
+    s[lo:hi] = 0
+    p[lo:hi] = 0
+    sc = torch.tensor([3.0, 7.0], dtype=torch.float64, device="cuda")  # beta = 3 / 7
+    num, den = sc.data_ptr(), sc.data_ptr() + 8
+    p1 = p.clone()
+    _lib.check(_lib.lib.gslm_xpby_dev(n, s.data_ptr(), num, den, p1.data_ptr(), _lib.stream_handle()))
+    y1 = prob.matvec(p1, prob.zeros()).clone()
+    p2 = p.clone()
+    y2 = prob.zeros()
+    prob.matvec_dot(p2, y2, None, pre=(s, num, den))
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)
+    assert torch.equal(y1, y2)
