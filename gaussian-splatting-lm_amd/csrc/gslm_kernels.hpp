@@ -19,8 +19,9 @@ struct GaussK {
   const float* rest;
   int64_t rest_stride;
   const float* colors;
+  int64_t rest_base = 0;  // rest holds Gaussians rest_base.. (an LDS-staged block slice) when nonzero
   __device__ __forceinline__ float sh(int64_t i, int k, int c) const {
-    return k == 0 ? dc[i * dc_stride + c] : rest[i * rest_stride + 3 * (k - 1) + c];
+    return k == 0 ? dc[i * dc_stride + c] : rest[(i - rest_base) * rest_stride + 3 * (k - 1) + c];
   }
 };
 

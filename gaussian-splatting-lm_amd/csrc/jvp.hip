@@ -16,7 +16,7 @@ constexpr int MATVEC_BATCH = 128;
 
 // p = s + beta p over this block's 256 Gaussians' slices of every group (coalesced, 8 loads in flight
 // per thread), and the flat tail by block 0.  Same arithmetic as k_xpby_dev (bitwise).
-__device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P) {
+__device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_rest) {
   const float b = (float)((*xp.num) / (*xp.den));
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t nv = min((int64_t)blockDim.x, P - i0);
@@ -37,7 +37,11 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
-        if (e < len) p[e] = sv[u] + b * pv[u];
+        if (e < len) {
+          const float r = sv[u] + b * pv[u];
+          p[e] = r;
+          if (k == 2) s_rest[e] = r;  // the SH-rest slice stays in LDS for the tangent below
+        }
       }
     }
   }
@@ -50,12 +54,18 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
                                                          const float4* __restrict__ rec,
                                                          const uint32_t* __restrict__ tiles,
                                                          float4* __restrict__ trec, XpbyK xp) {
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (XPBY) {
     // the direction this kernel reads is the updated one: each thread reads back only its own
-    // Gaussian's elements, all written by this block before the barrier
-    block_xpby(xp, g.P);
+    // Gaussian's elements, all written by this block before the barrier; its SH-rest tangent (the
+    // bulk of them, 3(M-1) floats at a 180-B stride) from the LDS copy instead of memory
+    block_xpby(xp, g.P, s_rest);
     __syncthreads();
+    if (t.rest) {
+      t.rest = s_rest;
+      t.rest_base = (int64_t)blockIdx.x * blockDim.x;
+    }
   }
   if (i >= g.P) return;
   if (tiles[i] == 0) return;  // never gathered by the render passes
@@ -253,11 +263,16 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
   XpbyK none{};
   const XpbyK& x = xp ? *xp : none;
   if (xp) {
+    if (t.rest && (t.rest != xp->p[2] || t.rest_stride != xp->w[2])) {
+      set_error("internal: fused xpby expects the tangent's SH-rest group to be p's");
+      return GSLM_ERR_INVALID;
+    }
+    const size_t lds = (size_t)256 * xp->w[2] * sizeof(float);
     if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
                          sb.trec, x);
     else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
                          sb.trec, x);
   } else {
     if (g.raw)
