@@ -57,6 +57,7 @@ size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
   b.vals1 = c.take<uint32_t>(N);
   b.hist = c.take<uint32_t>(sort_hist_bytes(N) / 4);
   b.ranges = c.take<uint2>(ntiles);
+  b.tile_order = c.take<uint32_t>(ntiles);
   b.end_bit = 1;
   while ((1ll << b.end_bit) < (long long)ntiles) ++b.end_bit;
   b.passes = (b.end_bit + 7) / 8;

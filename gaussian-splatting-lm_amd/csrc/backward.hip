@@ -20,6 +20,7 @@ namespace gslm {
 
 template <bool WITH_XY, bool WITH_INV>
 __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __restrict__ ranges,
+                                                     const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
                                                      const float4* __restrict__ rec, const uint2* __restrict__ rect,
                                                      const uint32_t* __restrict__ goff,
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   __shared__ uint64_t s_bits[16];
   __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV, TILE_PIX>()];
   __shared__ int s_misc[4];
-  const int tile = blockIdx.x;
+  const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
   int px, py;
@@ -242,10 +243,10 @@ int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
   const int ntiles = v.gx * v.gy;
   if (N == 0) return GSLM_OK;
   if (dL_dinv)
-    hipLaunchKernelGGL((k_render_bwd<true, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
+    hipLaunchKernelGGL((k_render_bwd<true, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
   else
-    hipLaunchKernelGGL((k_render_bwd<true, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
+    hipLaunchKernelGGL((k_render_bwd<true, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

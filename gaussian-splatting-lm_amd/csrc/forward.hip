@@ -63,6 +63,36 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
     }
 }
 
+// Launch order of the tile passes: tiles by descending list length (a longest-first schedule, so the
+// costliest tiles do not start last and set the kernel's tail).  One block; buckets of the length
+// (exact below 768 entries, 32-wide above), order inside a bucket arbitrary.  Only scheduling
+// changes: every tile's results are independent of when it runs.
+__global__ __launch_bounds__(1024) void k_tile_order(int ntiles, const uint2* __restrict__ ranges,
+                                                      uint32_t* __restrict__ order) {
+  __shared__ uint32_t s_cnt[1024];
+  const int tid = threadIdx.x;
+  s_cnt[tid] = 0u;
+  __syncthreads();
+  auto bucket = [&](int t) {
+    const uint32_t n = ranges[t].y - ranges[t].x;
+    return 1023u - (n < 768u ? n : min(1023u, 768u + ((n - 768u) >> 5)));  // heaviest first
+  };
+  for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
+  __syncthreads();
+  // exclusive scan of the 1024 bucket counts (Hillis-Steele on an inclusive copy)
+  uint32_t v = s_cnt[tid];
+  for (int o = 1; o < 1024; o <<= 1) {
+    __syncthreads();
+    const uint32_t a = tid >= o ? s_cnt[tid - o] : 0u;
+    __syncthreads();
+    s_cnt[tid] += a;
+  }
+  __syncthreads();
+  s_cnt[tid] -= v;  // exclusive
+  __syncthreads();
+  for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
+}
+
 // Gaussian ids of the sorted list (mask bits stripped), for gslm_inspect.
 __global__ __launch_bounds__(256) void k_point_ids(int64_t N, const uint32_t* __restrict__ pl, uint32_t* __restrict__ out) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -80,6 +110,7 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
 
 // renderCUDA forward.  Wave w holds the tile's 8x8 quadrant w (tile_pixel).
 __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
+                                                     const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
                                                      const float4* __restrict__ rec, float* __restrict__ out_color,
                                                      float* __restrict__ out_invdepth, float* __restrict__ final_T,
@@ -87,7 +118,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
   __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
   __shared__ float2 s_r2[TILE_PIX];
   __shared__ uint64_t s_bits[16];
-  const int tile = blockIdx.x;
+  const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x, w = tid >> 6;
   int px, py;
@@ -186,7 +217,11 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
                        gb.offsets, gb.tiles, gb.rect, gb.rec, bb.keys0, bb.vals0);
   GSLM_LAUNCH_CHECK();
-  if (N == 0) return GSLM_OK;
+  if (N == 0) {  // every range stays [0, 0); the tile passes still read a launch order
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
+    GSLM_LAUNCH_CHECK();
+    return GSLM_OK;
+  }
   bool alt = false;
   int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s);
   if (st != GSLM_OK) return st;
@@ -196,6 +231,8 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   }
   const unsigned nbN = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges);
+  GSLM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -211,7 +248,7 @@ int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
                       float* out_invdepth, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_render_fwd, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list, gb.rec,
+  hipLaunchKernelGGL(k_render_fwd, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list, gb.rec,
                      out_color, out_invdepth, ib.final_T, ib.n_contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

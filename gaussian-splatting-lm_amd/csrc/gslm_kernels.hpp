@@ -312,6 +312,7 @@ struct BinBufs {
   uint32_t* keys_sorted;  // sorted tile ids (aliases keys0 or keys1)
   uint32_t* hist;
   uint2* ranges;
+  uint32_t* tile_order;   // tiles by descending list length: the launch order of the tile passes
   int passes;
   int end_bit;
 };

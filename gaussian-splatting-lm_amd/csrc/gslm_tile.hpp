@@ -12,6 +12,11 @@
 
 namespace gslm {
 
+#if defined(GSLM_EXPERIMENT_COUNT) || defined(GSLM_EXPERIMENT_TIMELINE)
+static __device__ unsigned long long g_dbg[8];  // experiment builds only: tile-pass iteration counters
+static __device__ unsigned long long g_tile_t[3 * 65536];  // per-tile start / JVP end / VJP end (wall clock)
+#endif
+
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 __device__ __forceinline__ float dpp_f(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, BANK_MASK, true));
@@ -175,7 +180,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
   const int wmax = wave_max_u((int)st.last);
   if (lane == 0) s_misc[w] = wmax;
   __syncthreads();
-  const int n_eff = max(max(s_misc[0], s_misc[1]), max(s_misc[2], s_misc[3]));
+  // per-wave bound: wave w's lanes blend nothing at list positions >= wm[w]
+  const int wm0 = s_misc[0], wm1 = s_misc[1], wm2 = s_misc[2], wm3 = s_misc[3];
+  const int n_eff = max(max(wm0, wm1), max(wm2, wm3));
   {
     float z[NV];
 #pragma unroll
@@ -201,6 +208,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       const float4 r2 = rec[3 * (int64_t)g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
       my_slot = row_slot(goff[g], rect[g], tile_x, tile_y);
+      // and only the waves that still blend at this list position
+      const int pos = base - tid;
+      my_mask &= (pos < wm0 ? 1u : 0u) | (pos < wm1 ? 2u : 0u) | (pos < wm2 ? 4u : 0u) | (pos < wm3 ? 8u : 0u);
     }
     // which waves' quadrants this element can touch; wave w visits only its hits, and the combine below
     // takes zero for the others (exactly what a visit with no valid lane would have produced)
@@ -255,6 +265,16 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           gv[5] = G * dL_dalpha;
         }
         const bool any = __ballot(valid) != 0ull;
+#ifdef GSLM_EXPERIMENT_COUNT
+        {
+          const uint64_t vb = __ballot(valid);
+          if (lane == 0) {
+            atomicAdd(&g_dbg[2], 1ull);
+            atomicAdd(&g_dbg[3], (unsigned long long)__popcll(vb));
+            if (!any) atomicAdd(&g_dbg[4], 1ull);
+          }
+        }
+#endif
         if constexpr (NU <= 8) {
           // transposed reduction: value slot k ends in lanes 8k..8k+7; lane 8k stores it
           float rr = 0.f;

@@ -129,6 +129,15 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
         const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
+#ifdef GSLM_EXPERIMENT_COUNT
+        {
+          const uint64_t vb = __ballot(!(power > 0.0f) && alpha >= 1.0f / 255.0f);
+          if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_dbg[0], 1ull);
+            atomicAdd(&g_dbg[1], (unsigned long long)__popcll(vb));
+          }
+        }
+#endif
         if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
           float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
           if (WITH_XY) {
@@ -153,6 +162,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
 
 template <bool WITH_XY>
 __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __restrict__ ranges,
+                                                     const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
                                                      const float4* __restrict__ rec, const float4* __restrict__ trec,
                                                      const uint32_t* __restrict__ n_contrib,
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   __shared__ float2 s_r2[B], s_t2[B];
   __shared__ uint64_t s_bits[16];
   __shared__ int s_cnt[4];
-  const int tile = blockIdx.x;
+  const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
   int px, py;
@@ -185,6 +195,7 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
 // Fused (J^T W J) v for one view: JVP pass, per-pixel weight, VJP pass.
 template <bool WITH_XY>
 __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __restrict__ ranges,
+                                                        const uint32_t* __restrict__ tile_order,
                                                         const uint32_t* __restrict__ point_list,
                                                         const float4* __restrict__ rec, const float4* __restrict__ trec,
                                                         const uint2* __restrict__ rect,
@@ -210,7 +221,10 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   float2* s_t2 = reinterpret_cast<float2*>(s_union + 2 * B);
   float* s_acc = reinterpret_cast<float*>(s_union);
   int* s_misc = reinterpret_cast<int*>(s_union);
-  const int tile = blockIdx.x;
+  const int tile = (int)tile_order[blockIdx.x];
+#ifdef GSLM_EXPERIMENT_TIMELINE
+  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile] = wall_clock64();
+#endif
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
   int px, py;
@@ -244,8 +258,16 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
 #ifdef GSLM_EXPERIMENT_SKIP_VJP
   if (u0 + u1 + u2 == 12345.f) contrib[0] = make_float4(u0, u1, u2, 0.f);
 #else
+#ifdef GSLM_EXPERIMENT_TIMELINE
+  __syncthreads();
+  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 1] = wall_clock64();
+#endif
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
                                             rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib);
+#ifdef GSLM_EXPERIMENT_TIMELINE
+  __syncthreads();
+  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 2] = wall_clock64();
+#endif
 #endif
 }
 
@@ -294,10 +316,10 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
   const int ntiles = v.gx * v.gy;
   const bool xy = t.means3D != nullptr || m2t != nullptr;
   if (xy)
-    hipLaunchKernelGGL(k_render_jvp<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list, gb.rec,
+    hipLaunchKernelGGL(k_render_jvp<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list, gb.rec,
                        sb.trec, ib.n_contrib, out_color_t, out_inv_t);
   else
-    hipLaunchKernelGGL(k_render_jvp<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list, gb.rec,
+    hipLaunchKernelGGL(k_render_jvp<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list, gb.rec,
                        sb.trec, ib.n_contrib, out_color_t, out_inv_t);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
@@ -307,13 +329,27 @@ int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, co
                          const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (mask_xyz)
-    hipLaunchKernelGGL(k_render_matvec<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
+    hipLaunchKernelGGL(k_render_matvec<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
   else
-    hipLaunchKernelGGL(k_render_matvec<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.point_list,
+    hipLaunchKernelGGL(k_render_matvec<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
 
 }  // namespace gslm
+#if defined(GSLM_EXPERIMENT_COUNT) || defined(GSLM_EXPERIMENT_TIMELINE)
+extern "C" int gslm_dbg_tiles(unsigned long long* out, int n) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(gslm::g_tile_t), sizeof(unsigned long long) * 3 * n);
+  return 0;
+}
+extern "C" int gslm_dbg_read(unsigned long long* out, int reset) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(gslm::g_dbg), sizeof(unsigned long long) * 8);
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(gslm::g_dbg), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
