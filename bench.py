@@ -89,7 +89,7 @@ def main():
     del gt_prob, pert
 
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
-    prob = ShardedLMProblem(model, cams, bg, device=device)
+    prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device)
     prob.evaluate()
     g = prob.rhs(prob.zeros())
     torch.cuda.synchronize()
@@ -219,7 +219,8 @@ def main():
             "config": {"workload": f"LM CG iteration, {args.P} Gaussians SH{args.sh}, {args.views_per_gpu}x{W}x{H} "
                                    f"view(s) per GPU (BASELINE configs[2]; configs[3] at 8 GPUs)",
                        "P": args.P, "sh_degree": args.sh, "width": W, "height": H,
-                       "views_total": n_views, "parallelism": f"views sharded x{world_size}"},
+                       "views_total": n_views, "parallelism": f"views sharded x{world_size}",
+                       "exchange": prob.exchange if world_size > 1 else "none"},
             "cg_matvecs_per_s": args.steps / t_cg,
             "raster_mpix_s": mpix,
             "forward_ms_per_view": 1e3 * t_fwd / fsteps / max(len(prob.views), 1),

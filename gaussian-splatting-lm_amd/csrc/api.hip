@@ -376,12 +376,47 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
       (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
     return st;
+  if (stages & GSLM_STAGE_SCREEN) {
+    if (!mask_xyz || !opts->screen_out) {
+      set_error("matvec: GSLM_STAGE_SCREEN needs mask_xyz and opts->screen_out");
+      return GSLM_ERR_INVALID;
+    }
+    return launch_rowsum_screen(b.g, b.gb, b.sb, opts->screen_out, s);
+  }
   if (!(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
   double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
   if ((st = launch_gather_lm(b.v, b.g, b.gb, b.sb, make_gradk(y), make_gradk(vin), damp7,
                              (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, part, s)))
     return st;
   if (dot_out) return gslm_dot_finalize(part, (int32_t)((b.g.P + 255) / 256), dot_out, stream);
+  return GSLM_OK;
+}
+
+int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, const float* screen,
+                       const gslm_grads* vin, const gslm_grads* y, const gslm_matvec_opts* opts, void* stream) {
+  if (!views || nviews < 1 || nviews > 16 || !gi || !screen || !vin || !y) {
+    set_error("gather_screen: NULL argument or nviews outside 1..16");
+    return GSLM_ERR_INVALID;
+  }
+  ViewK vk[16];
+  GaussK g;
+  int st;
+  for (int b = 0; b < nviews; ++b)
+    if ((st = make_view(&views[b], gi->max_coeffs, &vk[b]))) return st;
+  if ((st = make_gauss(gi, &vk[0], &g, false))) return st;
+  if (!g.raw) { set_error("gather_screen: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
+  const int32_t stages = (opts && opts->stages) ? opts->stages : GSLM_STAGE_ALL;
+  const double* damp7 = opts ? opts->damp7 : nullptr;
+  double* dot_out = opts ? opts->dot_vy : nullptr;
+  if (dot_out && (!opts->dot_scratch || opts->dot_scratch_bytes < gslm_dot_scratch_bytes(g.P))) {
+    set_error("gather_screen: dot scratch too small");
+    return GSLM_ERR_CAPACITY;
+  }
+  double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
+  if ((st = launch_gather_screen(vk, nviews, g, screen, make_gradk(y), make_gradk(vin), damp7,
+                                 (stages & GSLM_STAGE_OVERWRITE) != 0, part, (hipStream_t)stream)))
+    return st;
+  if (dot_out) return gslm_dot_finalize(part, (int32_t)((g.P + 255) / 256), dot_out, stream);
   return GSLM_OK;
 }
 

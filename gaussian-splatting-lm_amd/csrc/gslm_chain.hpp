@@ -31,7 +31,7 @@ struct Geo {
 };
 
 template <bool RAW>
-__device__ __forceinline__ void compute_geo(const ViewK& v, const GaussK& g, int64_t i, const float4* rec, Geo& e) {
+__device__ __forceinline__ void compute_geo(const ViewK& v, const GaussK& g, int64_t i, uint32_t clamped, Geo& e) {
   e.x = g.means3D[3 * i + 0];
   e.y = g.means3D[3 * i + 1];
   e.z = g.means3D[3 * i + 2];
@@ -77,7 +77,7 @@ __device__ __forceinline__ void compute_geo(const ViewK& v, const GaussK& g, int
   e.dir[0] = dx / e.dirlen;
   e.dir[1] = dy / e.dirlen;
   e.dir[2] = dz / e.dirlen;
-  e.clamped = __float_as_uint(rec[3 * i + 2].z);
+  e.clamped = clamped;
 }
 
 // derivative of h = sqrt(max(2.5e-5, det0/det)) w.r.t. (a, b, c); zero when the max clamps
@@ -106,7 +106,7 @@ struct ChainOut {
 // Reverse mode: G2 = reduced screen-space gradient [x_pix, y_pix, conic a, b, c, opacity_eff, r, g, b, invdepth].
 template <bool RAW>
 __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64_t i, bool visible,
-                                          const float4* rec, const float G2[10], bool want_means, ChainOut& co) {
+                                          uint32_t clamped, const float G2[10], bool want_means, ChainOut& co) {
   co.dm2[0] = co.dm2[1] = 0.f;
   co.dop = 0.f;
 #pragma unroll
@@ -119,7 +119,7 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
   for (int k = 0; k < 16; ++k) co.dsh[k][0] = co.dsh[k][1] = co.dsh[k][2] = 0.f;
   if (!visible) return;
   Geo e;
-  compute_geo<RAW>(v, g, i, rec, e);
+  compute_geo<RAW>(v, g, i, clamped, e);
 
   // screen position (NDC means2D gradient, upstream ddelx_dx = 0.5 W)
   const float gpx = G2[0] * (0.5f * (float)v.W), gpy = G2[1] * (0.5f * (float)v.H);
@@ -325,9 +325,9 @@ __device__ __forceinline__ void write_grads(const GaussK& g, const GradK& o, int
 // out: [dx_pix, dy_pix, dconic a, b, c, dopacity_eff, dr, dg, db, dinvdepth]
 template <bool RAW>
 __device__ __forceinline__ void chain_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t,
-                                          int64_t i, const float4* rec, float T2[10]) {
+                                          int64_t i, uint32_t clamped, float T2[10]) {
   Geo e;
-  compute_geo<RAW>(v, g, i, rec, e);
+  compute_geo<RAW>(v, g, i, clamped, e);
   float dm[3] = {0.f, 0.f, 0.f};
   if (t.means3D)
 #pragma unroll

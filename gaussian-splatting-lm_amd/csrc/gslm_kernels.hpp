@@ -364,6 +364,9 @@ struct XpbyK {
 };
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                        const ScratchBufs& sb, const XpbyK* xp, hipStream_t s);
+int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s);
+int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, const GradK& y,
+                         const GradK& vin, const double* damp7, bool overwrite, double* dot_part, hipStream_t s);
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
   if (i >= g.P) return;
   if (tiles[i] == 0) return;  // never gathered by the render passes
   float T2[10];
-  chain_jvp<RAW>(v, g, t, m2t, i, rec, T2);
+  chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[3 * i + 2].z), T2);
   trec[3 * i + 0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
   trec[3 * i + 1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
   trec[3 * i + 2] = make_float4(T2[8], T2[9], 0.f, 0.f);

@@ -57,6 +57,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("dot_scratch", ctypes.c_void_p), ("dot_scratch_bytes", ctypes.c_size_t),
         ("xpby_s", ctypes.c_void_p), ("beta_num", ctypes.c_void_p), ("beta_den", ctypes.c_void_p),
         ("xpby_tail_v", ctypes.c_void_p), ("xpby_tail_s", ctypes.c_void_p), ("xpby_tail_n", ctypes.c_int64),
+        ("screen_out", ctypes.c_void_p),
     ]
 
 
@@ -95,6 +96,9 @@ EXPORTS = {
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_gather_screen": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
+                                          ctypes.c_void_p, ctypes.POINTER(GslmGrads), ctypes.POINTER(GslmGrads),
+                                          ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_cg_update": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]),

@@ -192,6 +192,67 @@ class LMProblem:
             y[e0:e1].zero_()
         return y
 
+    # -------------------------------------------------------------- view-sharded exchange (gslm.parallel)
+    def views_for(self, cams, pad_to=None):
+        """ctypes array of the gslm_view of every camera in `cams` (the whole sharded batch), padded
+        with copies of the last to `pad_to` entries (padded slots carry no screen data)."""
+        vs = [_lib.view_from_camera(c, self.bg, self.model.active_sh_degree) for c in cams]
+        vs += [vs[-1]] * max(0, (pad_to or len(vs)) - len(vs))
+        arr = (_lib.GslmView * len(vs))()
+        for k, vw in enumerate(vs):
+            arr[k] = vw
+        return arr
+
+    def screen_products(self, v, screen, pre=None):
+        """screen[b] = this rank's view b's per-Gaussian screen-space sums S_b^T W_b J_b v (P x 8,
+        GSLM_STAGE_SCREEN); pre as in matvec_dot (applied with the first view)."""
+        g = raw_gaussians(self.model)
+        vs = self.layout.grads_struct(v)
+        ys = self.layout.grads_struct(v)  # unused by the SCREEN stage
+        e0, e1 = self.layout.offsets["exposure"]
+        if pre is not None and not self.views:
+            s, num, den = pre
+            check(lib.gslm_xpby_dev(v.numel(), s.data_ptr(), num, den, v.data_ptr(), self.stream), "gslm_xpby_dev")
+        for b, vr in enumerate(self.views):
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = 1 | 2 | 16  # TANGENT | RENDER | SCREEN
+            opts.screen_out = screen[b].data_ptr()
+            if pre is not None and b == 0:
+                s, num, den = pre
+                ss = self.layout.grads_struct(s)
+                opts.xpby_s = ctypes.addressof(ss)
+                opts.beta_num, opts.beta_den = num, den
+                opts.xpby_tail_v = v.data_ptr() + 4 * e0
+                opts.xpby_tail_s = s.data_ptr() + 4 * e0
+                opts.xpby_tail_n = e1 - e0
+            check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                          self.weights[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                          vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                          ctypes.byref(ys), ctypes.byref(opts), self.stream), "gslm_matvec_view_ex")
+
+    def gather_screen(self, views, screen_all, v, y, dot_out=None, chunk=16):
+        """y = sum over all views b of C_b^T screen_all[b] + D v (exposure: D v only); <v, y> fused
+        into dot_out when given."""
+        g = raw_gaussians(self.model)
+        vs = self.layout.grads_struct(v)
+        ys = self.layout.grads_struct(y)
+        n = len(views)
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = (STAGE_ALL | STAGE_OVERWRITE) if c0 == 0 else STAGE_ALL
+            opts.damp7 = self._damps if c0 == 0 else None
+            if dot_out is not None and c1 == n:
+                opts.dot_vy = dot_out
+                opts.dot_scratch = self.dot_scratch.data_ptr()
+                opts.dot_scratch_bytes = self.dot_scratch.numel() * 8
+            vptr = ctypes.cast(ctypes.byref(views, c0 * ctypes.sizeof(_lib.GslmView)), ctypes.POINTER(_lib.GslmView))
+            check(lib.gslm_gather_screen(vptr, c1 - c0, ctypes.byref(g), screen_all[c0].data_ptr(), ctypes.byref(vs),
+                                         ctypes.byref(ys), ctypes.byref(opts), self.stream), "gslm_gather_screen")
+        e0, e1 = self.layout.offsets["exposure"]
+        torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
+        return y
+
     def damp_add(self, v, y):
         check(lib.gslm_damp_add(v.numel(), v.data_ptr(), self._bounds, self._damps, 7, y.data_ptr(), self.stream))
 

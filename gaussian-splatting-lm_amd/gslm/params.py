@@ -27,6 +27,11 @@ class ParamLayout:
             off += n
         self.numel = off
 
+    @property
+    def floats_per_gaussian(self):
+        """F = 11 + 3K: xyz 3, dc 3, rest 3(K-1), scaling 3, rotation 4, opacity 1."""
+        return 11 + 3 * self.K
+
     def views(self, flat):
         """dict group -> view of the flat tensor with the reference shape."""
         return {g: flat[a:b].view(self.shapes[g]) for g, (a, b) in self.offsets.items()}

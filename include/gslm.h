@@ -155,6 +155,8 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
 #define GSLM_STAGE_GATHER 4
 #define GSLM_STAGE_ALL 7
 #define GSLM_STAGE_OVERWRITE 8 /* GATHER writes y instead of accumulating into it */
+#define GSLM_STAGE_SCREEN 16   /* view-sharded exchange: write this view's per-Gaussian screen-space sums to
+                                  opts->screen_out (see gslm_gather_screen) instead of gathering into y */
 typedef struct gslm_matvec_opts {
   int32_t stages;         /* GSLM_STAGE_* bits; 0 means GSLM_STAGE_ALL (accumulate) */
   int32_t reserved;
@@ -175,11 +177,25 @@ typedef struct gslm_matvec_opts {
   float* xpby_tail_v;
   const float* xpby_tail_s;
   int64_t xpby_tail_n;
+  float* screen_out;      /* GSLM_STAGE_SCREEN output, P x 8 floats */
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                         int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
                         const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
+
+/* ---- view-sharded exchange (multi-GPU LM product), SURVEY 8(e) ----
+ * Instead of all-reducing the param-space partial J^T W J v (F = 59 floats per Gaussian at SH 3),
+ * every rank all-gathers per-view screen-space sums (8 floats per Gaussian per view) and applies the
+ * per-view chains itself.  GSLM_STAGE_SCREEN of gslm_matvec_view_ex writes, for Gaussian i of the
+ * view, screen[8 i .. 8 i + 7] = (dL/dconic a, b, c, dL/dopacity_eff, dL/dr, dL/dg, dL/db, flags),
+ * flags = bit 31 visible | bits 0-2 SH clamp mask (as float bits); xyz must be masked.
+ * gslm_gather_screen(views[0..nviews), screen[nviews][P][8]) then writes
+ *   y = sum_b J_b^T screen_b [+ D v]   (views summed in index order: identical on every rank),
+ * with opts->stages' OVERWRITE bit, damp7 and dot_vy as in gslm_matvec_view_ex.  nviews <= 16 per
+ * call (accumulate further calls).  Replaces the reduction of solver_functions.py:110-121. */
+int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const float* screen,
+                       const gslm_grads* v, const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
 
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
