@@ -56,10 +56,17 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # GSLM_BENCH_DIST=gloo rehearses the multi-rank path with several ranks on one GPU (host-staged
+    # collectives); the driver's runs use RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("GSLM_BENCH_DIST", "nccl")
+    dev_index = local_rank if backend == "nccl" else local_rank % max(torch.cuda.device_count(), 1)
     if world_size > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", dev_index)
 
     from gslm import _lib
     from gslm.cameras import orbit_cameras
