@@ -137,7 +137,11 @@ struct VjpPix {
   float dpix[3];    // dL/dcolor of this pixel
   float dinv;       // dL/dinvdepth of this pixel
   float bg_dot;     // <bg, dL/dpix>
-  float acc[3], acc_inv, last_alpha, last_color[3], last_inv;
+  // Upstream keeps the colour (and inverse depth) accumulated behind the current Gaussian per channel,
+  // but only its dot product with dL/dpix enters dL/dalpha; the recurrence is linear, so the dot
+  // itself is carried: accd = <acc, dL/dpix> (+ acc_inv dL/dinvdepth), last_cd = the previous
+  // Gaussian's <colour, dL/dpix> (+ invdepth term).
+  float accd, last_alpha, last_cd;
 };
 
 __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside, float T_final, uint32_t last,
@@ -148,11 +152,9 @@ __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside,
   s.dpix[0] = d0; s.dpix[1] = d1; s.dpix[2] = d2;
   s.dinv = dinv;
   s.bg_dot = (v.bg[0] * d0 + v.bg[1] * d1) + v.bg[2] * d2;
-  s.acc[0] = s.acc[1] = s.acc[2] = 0.f;
-  s.acc_inv = 0.f;
+  s.accd = 0.f;
   s.last_alpha = 0.f;
-  s.last_color[0] = s.last_color[1] = s.last_color[2] = 0.f;
-  s.last_inv = 0.f;
+  s.last_cd = 0.f;
 }
 
 // LDS floats needed by vjp_tile's per-wave partial sums: [wave][value slot][batch element], rows padded
@@ -231,26 +233,20 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
 #pragma unroll
         for (int q = 0; q < NV; ++q) gv[q] = 0.f;
         if (valid) {
+          // Only the primal tests above (power, alpha) must round exactly as the forward's; the
+          // derivative arithmetic below decides nothing and is contracted to FMAs.
+#pragma clang fp contract(fast)
           const float inv1ma = rcp_f(1.f - alpha);
           st.T = st.T * inv1ma;
           const float dchannel = alpha * st.T;
-          const float col[3] = {b.z, b.w, c.x};
-          float dL_dalpha = 0.f;
+          float cd = (b.z * st.dpix[0] + b.w * st.dpix[1]) + c.x * st.dpix[2];
+          if (WITH_INV) cd += c.y * st.dinv;
+          st.accd = st.accd + st.last_alpha * (st.last_cd - st.accd);
+          st.last_cd = cd;
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) {
-            st.acc[ch] = st.last_alpha * st.last_color[ch] + (1.f - st.last_alpha) * st.acc[ch];
-            st.last_color[ch] = col[ch];
-            dL_dalpha += (col[ch] - st.acc[ch]) * st.dpix[ch];
-            gv[6 + ch] = dchannel * st.dpix[ch];
-          }
-          if (WITH_INV) {
-            const float invd = c.y;
-            st.acc_inv = st.last_alpha * st.last_inv + (1.f - st.last_alpha) * st.acc_inv;
-            st.last_inv = invd;
-            dL_dalpha += (invd - st.acc_inv) * st.dinv;
-            gv[9] = dchannel * st.dinv;
-          }
-          dL_dalpha *= st.T;
+          for (int ch = 0; ch < 3; ++ch) gv[6 + ch] = dchannel * st.dpix[ch];
+          if (WITH_INV) gv[9] = dchannel * st.dinv;
+          float dL_dalpha = (cd - st.accd) * st.T;
           st.last_alpha = alpha;
           dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
           const float dL_dG = b.y * dL_dalpha;

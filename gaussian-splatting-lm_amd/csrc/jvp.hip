@@ -139,6 +139,8 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
         }
 #endif
         if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+          // the tangent arithmetic decides nothing (stop is frozen at the primal): FMA-contracted
+#pragma clang fp contract(fast)
           float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
           if (WITH_XY) {
             const float ddx = t0.x, ddy = t0.y;
