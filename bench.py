@@ -196,6 +196,10 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
+    # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
+    fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
+
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -237,11 +241,48 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms},
             "cpu_baseline": cpu,
+            "raster_fwd_bwd": fb,
         }
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_drop_in_fwd_bwd(device, W, H, s0, P=100_000, sh=3, reps=10):
+    """Forward + backward of one view through diff_gaussian_rasterization (activated leaves with
+    requires_grad, dL/dcolor ~ N(0, 1) seed 4: SURVEY §8(d) config 2)."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    m = synthetic_gaussians(P, sh, seed=0, s0=s0, device="cpu").to(device)
+    cam = orbit_cameras(1, W, H, seed=1)[0].to(device)
+    st = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+        bg=torch.zeros(3, device=device), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=sh, campos=cam.camera_center, prefiltered=False,
+        debug=False, antialiasing=False)
+    leaves = [t.detach().clone().requires_grad_(True) for t in
+              (m.get_xyz, m.get_opacity, m.get_scaling, m.get_rotation, m.get_features)]
+    means2D = torch.zeros(P, 3, device=device, requires_grad=True)
+    g4 = torch.Generator(device="cpu").manual_seed(4)
+    dcolor = torch.randn(3, H, W, generator=g4).to(device)
+    rast = GaussianRasterizer(raster_settings=st)
+
+    def step():
+        color, _, _ = rast(means3D=leaves[0], means2D=means2D, opacities=leaves[1], scales=leaves[2],
+                           rotations=leaves[3], shs=leaves[4])
+        color.backward(dcolor)
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    return {"config": f"{P} Gaussians SH{sh}, 1x{W}x{H} view, forward + backward via GaussianRasterizer "
+                      "(BASELINE configs[1])", "ms": 1e3 * t, "mpix_s": W * H / t / 1e6}
 
 
 if __name__ == "__main__":

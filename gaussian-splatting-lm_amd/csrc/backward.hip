@@ -29,10 +29,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
                                                      const uint32_t* __restrict__ n_contrib,
                                                      const float* __restrict__ dL_dcolor,
                                                      const float* __restrict__ dL_dinv, float4* __restrict__ rows) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
-  __shared__ float2 s_r2[TILE_PIX];
+  // 128-entry batches (as k_render_matvec): 24-26 KB of LDS per block -> 6 blocks per CU
+  constexpr int B = 128;
+  __shared__ float4 s_r0[B], s_r1[B];
+  __shared__ float2 s_r2[B];
   __shared__ uint64_t s_bits[16];
-  __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV, TILE_PIX>()];
+  __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV, B>()];
   __shared__ int s_misc[4];
   const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   }
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, d0, d1, d2, di);
-  vjp_tile<WITH_XY, WITH_INV, 3, TILE_PIX>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
+  vjp_tile<WITH_XY, WITH_INV, 3, B>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
                                  rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows);
 }
 
@@ -70,19 +72,56 @@ __device__ __forceinline__ void sum_rows(const float4* __restrict__ rows, uint32
   }
 }
 
+// Drop-in backward, one block per 256 consecutive Gaussians: block-cooperative row sums (their rows
+// are one contiguous range), the chain rule per thread, and the SH gradient -- 3M floats per Gaussian,
+// the bulk of the output -- staged through LDS and stored as contiguous wave segments (per-thread
+// stores at a 3M-float stride would touch a cache line per lane per store).
 template <bool RAW>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const float4* __restrict__ rec,
                                                          const uint32_t* __restrict__ tiles,
                                                          const uint32_t* __restrict__ goff,
                                                          const float4* __restrict__ rows, GradK out, int want_means) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.P) return;
-  const uint32_t n = tiles[i];
+  extern __shared__ __attribute__((aligned(16))) float s_buf[];  // row chunks, then [256][3M] SH grads
+  const int tid = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + tid;
+  const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
+  const uint32_t n = i < g.P ? tiles[i] : 0u;
   float G2[NV];
-  sum_rows<3>(rows, n ? goff[i] : 0u, n, G2);
+  {
+    const int64_t il = i0 + nvalid - 1;
+    const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
+    block_sum_rows<3>(rows, R0, R1, i < g.P ? goff[i] : R1, n, reinterpret_cast<float4*>(s_buf), G2);
+  }
+  const int nc = (v.D + 1) * (v.D + 1);
+  const bool sh_out = !g.colors && (out.dc || out.rest);
   ChainOut co;
-  chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, want_means != 0, co);
-  write_grads(g, out, i, co, v.M, (v.D + 1) * (v.D + 1), want_means != 0);
+  if (i < g.P) {
+    chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, want_means != 0, co);
+    write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
+  }
+  if (!sh_out) return;  // block-uniform
+  const int R = 3 * v.M;
+  if (i < g.P) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < v.M) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) s_buf[tid * R + 3 * k + ch] = k < nc ? co.dsh[k][ch] : 0.f;
+      }
+  }
+  __syncthreads();
+  const int acc = out.accumulate;
+  for (int64_t e = tid; e < nvalid * R; e += blockDim.x) {
+    const int64_t ii = e / R;
+    const int r = (int)(e - ii * R), k = r / 3, ch = r - 3 * k;
+    const int64_t gi = i0 + ii;
+    if (k == 0) {
+      if (out.dc) put(&out.dc[gi * out.dc_stride + ch], s_buf[e], acc);
+    } else if (out.rest) {
+      put(&out.rest[gi * out.rest_stride + 3 * (k - 1) + ch], s_buf[e], acc);
+    }
+  }
 }
 
 template <bool WANT_MEANS, int ROWF4>
@@ -128,11 +167,14 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
   (void)bb;
   if (g.P == 0) return GSLM_OK;
   const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const size_t sh_lds = (size_t)256 * 3 * g.M * sizeof(float);
+  const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
+  const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
   if (g.raw)
-    hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
                        sb.contrib, out, want_means ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
                        sb.contrib, out, want_means ? 1 : 0);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

@@ -278,7 +278,7 @@ __device__ __forceinline__ void put(float* p, float v, int acc) {
 
 // Store a ChainOut into the requested outputs (NULL pointers skipped).
 __device__ __forceinline__ void write_grads(const GaussK& g, const GradK& o, int64_t i, const ChainOut& co, int M,
-                                            int nc, bool want_means) {
+                                            int nc, bool want_means, bool skip_sh = false) {
   const int acc = o.accumulate;
   if (o.means2D) {
     put(&o.means2D[3 * i + 0], co.dm2[0], acc);
@@ -305,7 +305,7 @@ __device__ __forceinline__ void write_grads(const GaussK& g, const GradK& o, int
     if (o.colors)
 #pragma unroll
       for (int k = 0; k < 3; ++k) put(&o.colors[3 * i + k], co.dcol[k], acc);
-  } else {
+  } else if (!skip_sh) {
     if (o.dc)
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) put(&o.dc[i * o.dc_stride + ch], co.dsh[0][ch], acc);

@@ -286,17 +286,29 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           const int k = lane >> 3;
           if ((lane & 7) == 0 && k < NU) s_acc[(w * NU + k) * ACC_STRIDE + j] = rr;
         } else {
+          // slots 0..7 by the transposed reduction, the 1-2 extra slots (drop-in: means2D, invdepth)
+          // by lane-63 sums
+          constexpr int NX = NU - 8;
+          float rr = 0.f, ex[NX];
+#pragma unroll
+          for (int e = 0; e < NX; ++e) ex[e] = 0.f;
           if (any) {
+            float pv[8];
 #pragma unroll
             for (int q = 0; q < NV; ++q)
-              if (q_used<WITH_XY, WITH_INV>(q)) gv[q] = wave_sum_lane63(gv[q]);
-          }
-          if (lane == 63) {
+              if (q_used<WITH_XY, WITH_INV>(q)) {
+                const int sq = q_slot<WITH_XY, WITH_INV>(q);
+                if (sq < 8) pv[sq] = gv[q];
+                else ex[sq - 8] = gv[q];
+              }
+            rr = wave_reduce8_t(pv, lane);
 #pragma unroll
-            for (int q = 0; q < NV; ++q)
-              if (q_used<WITH_XY, WITH_INV>(q))
-                s_acc[(w * NU + q_slot<WITH_XY, WITH_INV>(q)) * ACC_STRIDE + j] = any ? gv[q] : 0.f;
+            for (int e = 0; e < NX; ++e) ex[e] = wave_sum_lane63(ex[e]);
           }
+          if ((lane & 7) == 0) s_acc[(w * NU + (lane >> 3)) * ACC_STRIDE + j] = rr;
+          if (lane == 63)
+#pragma unroll
+            for (int e = 0; e < NX; ++e) s_acc[(w * NU + 8 + e) * ACC_STRIDE + j] = ex[e];
         }
       }
     }
