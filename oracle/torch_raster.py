@@ -39,6 +39,18 @@ SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.37317633
          -0.4570457994644658, 1.445305721320277, -0.5900435899266435]
 
 
+def sqrt_ieee(x):
+    """sqrt whose VALUE is the correctly rounded float32 sqrt (IEEE 754, as the GPU's sqrtf and
+    upstream's CUDA sqrtf), with torch's derivative (straight-through, also under forward-AD).
+    torch's CPU Vectorized sqrt is not correctly rounded and its result depends on the host's
+    vector ISA (measured: 0.6% of random inputs on one AVX-512 host, 17% on another), which made
+    the restatement's radii host-dependent at the 1M-Gaussian scale."""
+    s = torch.sqrt(x)
+    base = s.detach()
+    exact = torch.from_numpy(np.sqrt(x.detach().cpu().numpy())).to(x.device)
+    return s + (exact - base)
+
+
 def eval_sh(deg, sh, dirs):
     """`utils/sh_utils.py:57-112` with sh laid out [P, K, 3] (reference `get_features` layout)."""
     result = SH_C0 * sh[:, 0]
@@ -77,8 +89,15 @@ def compute_cov3d(scales, scale_modifier, rotations):
     R = quat_to_rotmat(rotations)
     s = scale_modifier * scales
     L = R * s[:, None, :]
-    S = L @ L.transpose(1, 2)
-    return torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], dim=1)
+    # S = L L^T with every product and sum an explicit float32 elementwise op in a fixed association:
+    # a batched matmul (`L @ L.transpose`) is host-dependent (BLAS kernels may fuse multiply-adds or
+    # reorder on AVX-512 hosts), which made the restatement itself differ by ulps between machines.
+
+    def row_dot(i, j):
+        return (L[:, i, 0] * L[:, j, 0] + L[:, i, 1] * L[:, j, 1]) + L[:, i, 2] * L[:, j, 2]
+
+    return torch.stack([row_dot(0, 0), row_dot(0, 1), row_dot(0, 2), row_dot(1, 1), row_dot(1, 2), row_dot(2, 2)],
+                       dim=1)
 
 
 def _tp43(M, x, y, z, r):
@@ -120,9 +139,11 @@ def preprocess(means3D, means2D, opacities, shs, colors_precomp, scales, rotatio
     iny = ((tytz >= -limy) & (tytz <= limy)).detach()
     tcx = torch.where(inx, txtz * tz, (txtz.clamp(-limx, limx) * tz).detach())
     tcy = torch.where(iny, tytz * tz, (tytz.clamp(-limy, limy) * tz).detach())
-    J00 = fx / tz
+    # fx / tz as a tensor division: torch evaluates `python_scalar / tensor` as reciprocal(tensor) *
+    # scalar (two roundings), upstream divides once (computeCov2D); that differed in 26% of the J00s
+    J00 = torch.full_like(tz, fx) / tz
     J02 = -(fx * tcx) / (tz * tz)
-    J11 = fy / tz
+    J11 = torch.full_like(tz, fy) / tz
     J12 = -(fy * tcy) / (tz * tz)
     # A = J * W2C  (2x3); W2C[j][k] = V[4k + j]
     A0 = [J00 * V[4 * k + 0] + J02 * V[4 * k + 2] for k in range(3)]
@@ -143,7 +164,7 @@ def preprocess(means3D, means2D, opacities, shs, colors_precomp, scales, rotatio
     c11 = c11 + 0.3
     det = c00 * c11 - c01 * c01
     if st.antialiasing:
-        h = torch.sqrt(torch.clamp_min(det0 / det, 0.000025))
+        h = sqrt_ieee(torch.clamp_min(det0 / det, 0.000025))
     else:
         h = torch.ones_like(det)
     det_ok = (det != 0).detach()
@@ -154,8 +175,8 @@ def preprocess(means3D, means2D, opacities, shs, colors_precomp, scales, rotatio
     # 6. radius
     with torch.no_grad():
         mid = 0.5 * (c00 + c11)
-        lam1 = mid + torch.sqrt(torch.clamp_min(mid * mid - det, 0.1))
-        radius = torch.ceil(3.0 * torch.sqrt(lam1))
+        lam1 = mid + sqrt_ieee(torch.clamp_min(mid * mid - det, 0.1))
+        radius = torch.ceil(3.0 * sqrt_ieee(lam1))
 
     # 7. screen position and rect
     # ndc2Pix is evaluated in double upstream (`((v + 1.0) * S - 1.0) * 0.5` with double literals)
@@ -176,7 +197,7 @@ def preprocess(means3D, means2D, opacities, shs, colors_precomp, scales, rotatio
     if colors_precomp is None:
         campos = st.campos.reshape(-1).to(means3D.dtype)
         d = means3D - campos[None, :]
-        d = d / torch.sqrt((d * d).sum(dim=1, keepdim=True))
+        d = d / sqrt_ieee((d[:, 0:1] * d[:, 0:1] + d[:, 1:2] * d[:, 1:2]) + d[:, 2:3] * d[:, 2:3])
         res = eval_sh(st.sh_degree, shs, d) + 0.5
         clamped = (res < 0).detach()
         rgb = torch.clamp_min(res, 0.0)
@@ -186,7 +207,7 @@ def preprocess(means3D, means2D, opacities, shs, colors_precomp, scales, rotatio
 
     radii = torch.where(visible, radius, torch.zeros_like(radius)).to(torch.int32)
     tiles = torch.where(visible, area, torch.zeros_like(area))
-    return dict(xy=xy, depth=tz, conic=conic, opacity=opacities[:, 0] * h, rgb=rgb, clamped=clamped,
+    return dict(xy=xy, depth=tz, conic=conic, cov2d=torch.stack([c00, c01, c11], dim=1), opacity=opacities[:, 0] * h, rgb=rgb, clamped=clamped,
                 radii=radii, tiles_touched=tiles, visible=visible,
                 rect=torch.stack([rmin_x, rmin_y, rmax_x, rmax_y], dim=1), grid=(gx, gy))
 
