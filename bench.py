@@ -151,6 +151,7 @@ def main():
     def stage(mask):
         opts = _lib.GslmMatvecOpts()
         opts.stages = mask | (8 if mask == 4 else 0)  # the gather in its CG form: overwrite + D v
+        opts.flags = 1 if mask == 2 else 0  # GSLM_MV_TAIL_CLEAN: as inside the CG loop (first call below)
         opts.damp7 = prob._damps if mask == 4 else None
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
                                       prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
@@ -158,6 +159,12 @@ def main():
                                       ctypes.byref(ys), ctypes.byref(opts), prob.stream))
 
     stage(1)
+    opts0 = _lib.GslmMatvecOpts()
+    opts0.stages = 2  # RENDER once with the tail rows written: the state every CG iteration after the first sees
+    check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs), prob.weights[0].data_ptr(),
+                                  1, vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
+                                  vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts0),
+                                  prob.stream))
     stage(2)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = max(args.steps, 5)

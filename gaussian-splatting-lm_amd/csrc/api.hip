@@ -63,6 +63,7 @@ size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
   b.passes = (b.end_bit + 7) / 8;
   b.point_list = (b.passes & 1) ? b.vals1 : b.vals0;
   b.keys_sorted = (b.passes & 1) ? b.keys1 : b.keys0;
+  b.slots = (b.passes & 1) ? b.keys0 : b.keys1;
   if (o) *o = b;
   return c.off;
 }
@@ -374,7 +375,8 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
       (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s)))
     return st;
   if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
-      (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, pixel_weight, mask_xyz != 0, s)))
+      (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, N, pixel_weight, mask_xyz != 0,
+                                 opts && (opts->flags & GSLM_MV_TAIL_CLEAN), s)))
     return st;
   if (stages & GSLM_STAGE_SCREEN) {
     if (!mask_xyz || !opts->screen_out) {

@@ -23,8 +23,9 @@ template <bool WITH_XY, bool WITH_INV>
 __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
-                                                     const float4* __restrict__ rec, const uint2* __restrict__ rect,
-                                                     const uint32_t* __restrict__ goff,
+                                                     const float4* __restrict__ rec,
+                                                     const uint32_t* __restrict__ slots,
+                                                     const uint2* __restrict__ rect, const uint32_t* __restrict__ goff,
                                                      const float* __restrict__ final_T,
                                                      const uint32_t* __restrict__ n_contrib,
                                                      const float* __restrict__ dL_dcolor,
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, d0, d1, d2, di);
   vjp_tile<WITH_XY, WITH_INV, 3, B>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
-                                 rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows);
+                                 slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows, true);
 }
 
 template <int ROWF4>
@@ -154,10 +155,10 @@ int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
   if (N == 0) return GSLM_OK;
   if (dL_dinv)
     hipLaunchKernelGGL((k_render_bwd<true, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
+                       gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
   else
     hipLaunchKernelGGL((k_render_bwd<true, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
+                       gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

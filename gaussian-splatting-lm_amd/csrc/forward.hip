@@ -108,6 +108,29 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
   if (k == N - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
 }
 
+// Gradient-row slot of every sorted entry (row_slot), so the tile passes read it coalesced instead
+// of gathering goff / rect per entry.  The goff / rect gathers here are random over 12 B/Gaussian
+// (~90 us at 1M Gaussians / 4.9M entries), so the fused LM product computes the slots once per
+// geometry (GSLM_MV_TAIL_CLEAN protocol) and the forward does not.
+__global__ __launch_bounds__(256) void k_row_slots(int64_t N, int gx, const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ point_list,
+                                                    const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
+                                                    uint32_t* __restrict__ slots) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const uint32_t t = keys[k];
+  const uint32_t g = pl_id(point_list[k]);
+  slots[k] = row_slot(goff[g], rect[g], (int)(t % (uint32_t)gx), (int)(t / (uint32_t)gx));
+}
+
+int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s) {
+  if (N <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_row_slots, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, v.gx, bb.keys_sorted,
+                     bb.point_list, gb.goff, gb.rect, bb.slots);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 // renderCUDA forward.  Wave w holds the tile's 8x8 quadrant w (tile_pixel).
 __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,

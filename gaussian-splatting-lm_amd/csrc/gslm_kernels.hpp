@@ -313,6 +313,9 @@ struct BinBufs {
   uint32_t* hist;
   uint2* ranges;
   uint32_t* tile_order;   // tiles by descending list length: the launch order of the tile passes
+  uint32_t* slots;        // [N] gradient-row slot of each sorted entry (row_slot, k_row_slots), in the
+                          // sort's free ping-pong key buffer; valid only once the fused LM product
+                          // computed it for the current binning
   int passes;
   int end_bit;
 };
@@ -338,6 +341,7 @@ size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
 
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
 int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
+int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s);
@@ -371,7 +375,8 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
-                         const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s);
+                         const ScratchBufs& sb, int64_t N, const float* weight, bool mask_xyz, bool tail_clean,
+                         hipStream_t s);
 int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
                      const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
                      hipStream_t s);

@@ -169,10 +169,11 @@ constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * acc_st
 template <bool WITH_XY, bool WITH_INV, int ROWF4, int BATCH>
 __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint2 range, const uint32_t* __restrict__ point_list,
-                                         const float4* __restrict__ rec, const uint2* __restrict__ rect,
-                                         const uint32_t* __restrict__ goff, float4* s_r0, float4* s_r1,
+                                         const float4* __restrict__ rec, const uint32_t* __restrict__ slots,
+                                         const uint2* __restrict__ rect, const uint32_t* __restrict__ goff,
+                                         float4* s_r0, float4* s_r1,
                                          float2* s_r2, uint64_t* s_bits, float* s_acc, int* s_misc,
-                                         float4* __restrict__ rows) {
+                                         float4* __restrict__ rows, bool write_tail) {
   constexpr int NU = n_used<WITH_XY, WITH_INV>();
   constexpr int ACC_STRIDE = acc_stride<BATCH>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -185,13 +186,19 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
   // per-wave bound: wave w's lanes blend nothing at list positions >= wm[w]
   const int wm0 = s_misc[0], wm1 = s_misc[1], wm2 = s_misc[2], wm3 = s_misc[3];
   const int n_eff = max(max(wm0, wm1), max(wm2, wm3));
-  {
+  if (write_tail) {
     float z[NV];
 #pragma unroll
     for (int q = 0; q < NV; ++q) z[q] = 0.f;
     for (int64_t k = (int64_t)range.x + n_eff + tid; k < (int64_t)range.y; k += TILE_PIX) {
-      const uint32_t g = pl_id(point_list[k]);
-      store_row<ROWF4>(rows, row_slot(goff[g], rect[g], tile_x, tile_y), z);
+      uint32_t slot;
+      if (slots) {
+        slot = slots[k];
+      } else {
+        const uint32_t g = pl_id(point_list[k]);
+        slot = row_slot(goff[g], rect[g], tile_x, tile_y);
+      }
+      store_row<ROWF4>(rows, slot, z);
     }
   }
   const int rounds = (n_eff + BATCH - 1) / BATCH;
@@ -209,7 +216,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       s_r1[tid] = rec[3 * (int64_t)g + 1];
       const float4 r2 = rec[3 * (int64_t)g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
-      my_slot = row_slot(goff[g], rect[g], tile_x, tile_y);
+      my_slot = slots ? slots[range.x + base - tid] : row_slot(goff[g], rect[g], tile_x, tile_y);
       // and only the waves that still blend at this list position
       const int pos = base - tid;
       my_mask &= (pos < wm0 ? 1u : 0u) | (pos < wm1 ? 2u : 0u) | (pos < wm2 ? 4u : 0u) | (pos < wm3 ? 8u : 0u);

@@ -200,11 +200,13 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
                                                         const uint32_t* __restrict__ tile_order,
                                                         const uint32_t* __restrict__ point_list,
                                                         const float4* __restrict__ rec, const float4* __restrict__ trec,
+                                                        const uint32_t* __restrict__ slots,
                                                         const uint2* __restrict__ rect,
                                                         const uint32_t* __restrict__ goff,
                                                         const float* __restrict__ final_T,
                                                         const uint32_t* __restrict__ n_contrib,
-                                                        const float* __restrict__ weight, float4* __restrict__ contrib) {
+                                                        const float* __restrict__ weight, float4* __restrict__ contrib,
+                                                        int write_tail) {
   // 128-entry batches: 19.7 KB of LDS per block -> 8 blocks (VGPR-limited to 6 waves per SIMD) per CU,
   // the occupancy this latency-bound pass needs
   constexpr int B = MATVEC_BATCH;
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 1] = wall_clock64();
 #endif
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
-                                            rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib);
+                                            slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib, write_tail != 0);
 #ifdef GSLM_EXPERIMENT_TIMELINE
   __syncthreads();
   if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 2] = wall_clock64();
@@ -328,14 +330,22 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
 }
 
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
-                         const ScratchBufs& sb, const float* weight, bool mask_xyz, hipStream_t s) {
+                         const ScratchBufs& sb, int64_t N, const float* weight, bool mask_xyz, bool tail_clean,
+                         hipStream_t s) {
   const int ntiles = v.gx * v.gy;
+  // the per-entry row slots live with the tail rows: computed by the first product on a geometry
+  if (!tail_clean) {
+    const int st = launch_row_slots(v, gb, bb, N, s);
+    if (st) return st;
+  }
   if (mask_xyz)
     hipLaunchKernelGGL(k_render_matvec<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
+                       gb.rec, sb.trec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib,
+                       tail_clean ? 0 : 1);
   else
     hipLaunchKernelGGL(k_render_matvec<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, sb.trec, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib);
+                       gb.rec, sb.trec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib,
+                       tail_clean ? 0 : 1);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

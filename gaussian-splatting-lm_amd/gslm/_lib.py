@@ -52,7 +52,7 @@ class GslmGrads(ctypes.Structure):
 
 class GslmMatvecOpts(ctypes.Structure):
     _fields_ = [
-        ("stages", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("stages", ctypes.c_int32), ("flags", ctypes.c_int32),
         ("damp7", ctypes.POINTER(ctypes.c_double)), ("dot_vy", ctypes.c_void_p),
         ("dot_scratch", ctypes.c_void_p), ("dot_scratch_bytes", ctypes.c_size_t),
         ("xpby_s", ctypes.c_void_p), ("beta_num", ctypes.c_void_p), ("beta_den", ctypes.c_void_p),

@@ -27,6 +27,7 @@ from gslm.params import GROUPS, ParamLayout, raw_gaussians
 # train_jvp.py:229-235
 STAGE_ALL = 7
 STAGE_OVERWRITE = 8
+MV_TAIL_CLEAN = 1  # gslm_matvec_opts.flags: GSLM_MV_TAIL_CLEAN
 
 DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
                 "opacity": 5e-2, "exposure": 1e1}
@@ -41,10 +42,14 @@ class ViewRaster:
         self.device = device
         self.N = 0
         self.geom = self.binning = self.image = self.scratch = None
+        # the scratch's gradient rows of never-blended entries hold the zeros of an earlier fused
+        # product on the current geometry (GSLM_MV_TAIL_CLEAN): false after a forward or a backward
+        self.tail_clean = False
 
     def forward(self, g, stream):
         P = g.P
         dev = self.device
+        self.tail_clean = False
         if self.geom is None or self.geom.numel() < lib.gslm_geom_bytes(P):
             self.geom = _lib.u8(lib.gslm_geom_bytes(P), dev)
             self.image = _lib.u8(lib.gslm_image_bytes(self.H, self.W), dev)
@@ -124,6 +129,7 @@ class LMProblem:
             check(lib.gslm_backward(ctypes.byref(vr.view), ctypes.byref(g), vr.geom.data_ptr(), vr.binning.data_ptr(),
                                     vr.N, vr.image.data_ptr(), dL.data_ptr(), None, vr.scratch.data_ptr(),
                                     vr.scratch.numel(), ctypes.byref(grads), self.stream), "gslm_backward")
+            vr.tail_clean = False
         self._apply_mask(out)
         return out
 
@@ -168,6 +174,7 @@ class LMProblem:
         for b, vr in enumerate(self.views):
             opts = _lib.GslmMatvecOpts()
             opts.stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
+            opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
             opts.damp7 = self._damps if (damp and b == 0) else None
             if pre is not None and b == 0:
                 s, num, den = pre
@@ -186,6 +193,7 @@ class LMProblem:
                                           vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
                                           vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts), self.stream),
                   "gslm_matvec_view_ex")
+            vr.tail_clean = True
         if damp:
             torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
         else:
@@ -216,6 +224,7 @@ class LMProblem:
         for b, vr in enumerate(self.views):
             opts = _lib.GslmMatvecOpts()
             opts.stages = 1 | 2 | 16  # TANGENT | RENDER | SCREEN
+            opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
             opts.screen_out = screen[b].data_ptr()
             if pre is not None and b == 0:
                 s, num, den = pre
@@ -229,6 +238,7 @@ class LMProblem:
                                           self.weights[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
                                           ctypes.byref(ys), ctypes.byref(opts), self.stream), "gslm_matvec_view_ex")
+            vr.tail_clean = True
 
     def gather_screen(self, views, screen_all, v, y, dot_out=None, chunk=16):
         """y = sum over all views b of C_b^T screen_all[b] + D v (exposure: D v only); <v, y> fused

@@ -157,9 +157,16 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
 #define GSLM_STAGE_OVERWRITE 8 /* GATHER writes y instead of accumulating into it */
 #define GSLM_STAGE_SCREEN 16   /* view-sharded exchange: write this view's per-Gaussian screen-space sums to
                                   opts->screen_out (see gslm_gather_screen) instead of gathering into y */
+/* opts->flags: GSLM_MV_TAIL_CLEAN -- the caller guarantees that the scratch's gradient rows of
+ * never-blended list entries (positions past every pixel's n_contrib in their tile) still hold the
+ * zeros an earlier RENDER stage wrote for this same geometry / binning (no forward, backward or
+ * other use of the scratch or the binning buffer since); RENDER then skips re-writing them and
+ * re-deriving each sorted entry's row slot (kept in the binning buffer's free sort ping-pong half).
+ * Both depend on the geometry only, so an LM step's CG loop pays for them once. */
+#define GSLM_MV_TAIL_CLEAN 1
 typedef struct gslm_matvec_opts {
   int32_t stages;         /* GSLM_STAGE_* bits; 0 means GSLM_STAGE_ALL (accumulate) */
-  int32_t reserved;
+  int32_t flags;          /* GSLM_MV_* bits */
   const double* damp7;    /* host array (GaussianModelDampMatrix order: xyz, dc, rest, scaling, rotation,
                              opacity, exposure) or NULL; when set GATHER also adds D v (exposure untouched) */
   double* dot_vy;         /* device double or NULL: receives <v, y> over the gathered groups after GATHER */

@@ -149,3 +149,27 @@ def test_fused_xpby_matches_separate():
     torch.cuda.synchronize()
     assert torch.equal(p1, p2)
     assert torch.equal(y1, y2)
+
+
+def test_tail_rows_written_once_per_geometry():
+    """GSLM_MV_TAIL_CLEAN: the zero rows of never-blended entries are written by the first product on a
+    geometry and skipped afterwards.  A scratch poisoned with NaN before the first product, a second
+    product reusing the tail, and a product after rhs() (whose backward reuses the scratch with
+    48-byte rows) must all equal a fresh problem's product bitwise."""
+    from gslm.lm import LMProblem
+    d, m, cams = _load()
+    v = torch.from_numpy(d["v"]).cuda()
+    fresh = LMProblem(m, cams, torch.zeros(3))
+    fresh.evaluate()
+    ref = fresh.matvec(v, fresh.zeros()).clone()
+    prob = LMProblem(m, cams, torch.zeros(3))
+    prob.evaluate()
+    for vr in prob.views:
+        vr.scratch.view(torch.float32)[: vr.scratch.numel() // 4].fill_(float("nan"))
+    y1 = prob.matvec(v, prob.zeros()).clone()
+    assert all(vr.tail_clean for vr in prob.views)
+    y2 = prob.matvec(v, prob.zeros()).clone()
+    prob.rhs(prob.zeros())
+    assert not any(vr.tail_clean for vr in prob.views)
+    y3 = prob.matvec(v, prob.zeros())
+    assert torch.equal(y1, ref) and torch.equal(y2, ref) and torch.equal(y3, ref)
