@@ -1,0 +1,145 @@
+// gather.hip -- per-Gaussian side of the VJP: row sums and the chain rule to the parameters.
+//
+//   k_preprocess_bwd   one block per 256 consecutive Gaussians: sums their contiguous rows and
+//                      chains the screen-space gradient to means3D / scales / rotations / SH /
+//                      opacity (or to cov3D_precomp / colors_precomp), fusing the activation
+//                      derivatives when the inputs are raw GaussianModel leaves (drop-in backward).
+//   k_gather_lm        the LM specialisation (raw leaves, SH colours): writes the flat param-space
+//                      vector directly, overwrite or accumulate, with the damping term D v fused in,
+//                      SH-rest stores staged through LDS so every store instruction is a contiguous
+//                      256-B wave segment.
+// Compiled apart from the tile passes: these keep clang's SLP vectoriser (Makefile).
+#include "gslm_tile.hpp"
+#include "gslm_chain.hpp"
+#include "gslm_gather.hpp"
+
+namespace gslm {
+
+template <int ROWF4>
+__device__ __forceinline__ void sum_rows(const float4* __restrict__ rows, uint32_t off, uint32_t n, float G2[NV]) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q) G2[q] = 0.f;
+  for (uint32_t t = 0; t < n; ++t) {
+    float r[NV];
+    load_row<ROWF4>(rows, (size_t)off + t, r);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) G2[q] += r[q];
+  }
+}
+
+// Drop-in backward, one block per 256 consecutive Gaussians: block-cooperative row sums (their rows
+// are one contiguous range), the chain rule per thread, and the SH gradient -- 3M floats per Gaussian,
+// the bulk of the output -- staged through LDS and stored as contiguous wave segments (per-thread
+// stores at a 3M-float stride would touch a cache line per lane per store).
+template <bool RAW>
+__global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const float4* __restrict__ rec,
+                                                         const uint32_t* __restrict__ tiles,
+                                                         const uint32_t* __restrict__ goff,
+                                                         const float4* __restrict__ rows, GradK out, int want_means) {
+  extern __shared__ __attribute__((aligned(16))) float s_buf[];  // row chunks, then [256][3M] SH grads
+  const int tid = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + tid;
+  const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
+  const uint32_t n = i < g.P ? tiles[i] : 0u;
+  float G2[NV];
+  {
+    const int64_t il = i0 + nvalid - 1;
+    const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
+    block_sum_rows<3>(rows, R0, R1, i < g.P ? goff[i] : R1, n, reinterpret_cast<float4*>(s_buf), G2);
+  }
+  const int nc = (v.D + 1) * (v.D + 1);
+  const bool sh_out = !g.colors && (out.dc || out.rest);
+  ChainOut co;
+  if (i < g.P) {
+    chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, want_means != 0, co);
+    write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
+  }
+  if (!sh_out) return;  // block-uniform
+  const int R = 3 * v.M;
+  if (i < g.P) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < v.M) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) s_buf[tid * R + 3 * k + ch] = k < nc ? co.dsh[k][ch] : 0.f;
+      }
+  }
+  __syncthreads();
+  const int acc = out.accumulate;
+  for (int64_t e = tid; e < nvalid * R; e += blockDim.x) {
+    const int64_t ii = e / R;
+    const int r = (int)(e - ii * R), k = r / 3, ch = r - 3 * k;
+    const int64_t gi = i0 + ii;
+    if (k == 0) {
+      if (out.dc) put(&out.dc[gi * out.dc_stride + ch], s_buf[e], acc);
+    } else if (out.rest) {
+      put(&out.rest[gi * out.rest_stride + 3 * (k - 1) + ch], s_buf[e], acc);
+    }
+  }
+}
+
+template <bool WANT_MEANS, int ROWF4>
+__global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
+                                                    const uint32_t* __restrict__ tiles,
+                                                    const uint32_t* __restrict__ goff,
+                                                    const float4* __restrict__ rows, FlatK o) {
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(K-1)], first the row chunks
+  __shared__ double s_dot[4];
+  const int tid = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + tid;
+  const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
+  const uint32_t n = i < g.P ? tiles[i] : 0u;
+  float G2[NV];
+  {
+    const int64_t il = i0 + nvalid - 1;
+    const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
+    block_sum_rows<ROWF4>(rows, R0, R1, i < g.P ? goff[i] : R1, n, reinterpret_cast<float4*>(s_rest), G2);
+  }
+  ChainOut co;
+  if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, WANT_MEANS, co);
+  lm_epilogue<WANT_MEANS>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
+}
+
+// ---------------------------------------------------------------- launchers
+int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, const BinBufs& bb,
+                          const ScratchBufs& sb, const GradK& out, bool want_means, hipStream_t s) {
+  (void)bb;
+  if (g.P == 0) return GSLM_OK;
+  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const size_t sh_lds = (size_t)256 * 3 * g.M * sizeof(float);
+  const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
+  const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
+  if (g.raw)
+    hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.contrib, out, want_means ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.contrib, out, want_means ? 1 : 0);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
+                     const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
+                     hipStream_t s) {
+  if (g.P == 0) return GSLM_OK;
+  FlatK o;
+  const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o);
+  if (st) return st;
+  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const size_t rest_lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float);
+  const size_t chunk_lds = (size_t)GATHER_CHUNK * (mask_xyz ? 2 : 3) * sizeof(float4);
+  const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
+  if (mask_xyz)
+    hipLaunchKernelGGL((k_gather_lm<false, 2>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.contrib, o);
+  else
+    hipLaunchKernelGGL((k_gather_lm<true, 3>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.contrib, o);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+}  // namespace gslm

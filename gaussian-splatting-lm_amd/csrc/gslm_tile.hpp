@@ -236,6 +236,14 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
         const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
+        // <colour, dL/dpix> for every lane, so the record's colour is read with the rest of it (one LDS
+        // round trip per entry instead of a second one inside the valid branch)
+        float cd;
+        {
+#pragma clang fp contract(fast)
+          cd = (b.z * st.dpix[0] + b.w * st.dpix[1]) + c.x * st.dpix[2];
+          if (WITH_INV) cd += c.y * st.dinv;
+        }
         float gv[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) gv[q] = 0.f;
@@ -246,8 +254,6 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           const float inv1ma = rcp_f(1.f - alpha);
           st.T = st.T * inv1ma;
           const float dchannel = alpha * st.T;
-          float cd = (b.z * st.dpix[0] + b.w * st.dpix[1]) + c.x * st.dpix[2];
-          if (WITH_INV) cd += c.y * st.dinv;
           st.accd = st.accd + st.last_alpha * (st.last_cd - st.accd);
           st.last_cd = cd;
 #pragma unroll

@@ -1,7 +1,6 @@
-// jvp.hip -- forward-mode tangent of the rasterizer and the fused LM normal-equations product.
+// jvp.hip -- tile passes of the forward-mode tangent and of the fused LM normal-equations product
+// (the per-Gaussian tangent records come from tangent.hip).
 //
-//   k_preprocess_jvp   one thread per visible Gaussian: tangent render record (48 B) from the
-//                      input tangents (chain_jvp, exact transpose of chain_vjp).
 //   k_render_jvp       per tile, front-to-back over the *primal's* sorted list (no re-sort), the
 //                      skip/stop decisions frozen at the primal (bounded by n_contrib):
 //                        dC += drgb a T + rgb (da T + a dT),  dT <- dT (1 - a) - T da.
@@ -13,68 +12,6 @@
 namespace gslm {
 
 constexpr int MATVEC_BATCH = 128;
-
-// p = s + beta p over this block's 256 Gaussians' slices of every group (coalesced, 8 loads in flight
-// per thread), and the flat tail by block 0.  Same arithmetic as k_xpby_dev (bitwise).
-__device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_rest) {
-  const float b = (float)((*xp.num) / (*xp.den));
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t nv = min((int64_t)blockDim.x, P - i0);
-  constexpr int U = 8;
-  for (int k = 0; k < 6; ++k) {
-    if (!xp.p[k]) continue;
-    float* p = xp.p[k] + i0 * xp.w[k];
-    const float* s = xp.s[k] + i0 * xp.w[k];
-    const int64_t len = nv * xp.w[k];
-    for (int64_t e0 = 0; e0 < len; e0 += (int64_t)U * blockDim.x) {
-      float sv[U], pv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
-        sv[u] = e < len ? s[e] : 0.f;
-        pv[u] = e < len ? p[e] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
-        if (e < len) {
-          const float r = sv[u] + b * pv[u];
-          p[e] = r;
-          if (k == 2) s_rest[e] = r;  // the SH-rest slice stays in LDS for the tangent below
-        }
-      }
-    }
-  }
-  if (blockIdx.x == 0 && xp.tail_p)
-    for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) xp.tail_p[e] = xp.tail_s[e] + b * xp.tail_p[e];
-}
-
-template <bool RAW, bool XPBY>
-__global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
-                                                         const float4* __restrict__ rec,
-                                                         const uint32_t* __restrict__ tiles,
-                                                         float4* __restrict__ trec, XpbyK xp) {
-  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (XPBY) {
-    // the direction this kernel reads is the updated one: each thread reads back only its own
-    // Gaussian's elements, all written by this block before the barrier; its SH-rest tangent (the
-    // bulk of them, 3(M-1) floats at a 180-B stride) from the LDS copy instead of memory
-    block_xpby(xp, g.P, s_rest);
-    __syncthreads();
-    if (t.rest) {
-      t.rest = s_rest;
-      t.rest_base = (int64_t)blockIdx.x * blockDim.x;
-    }
-  }
-  if (i >= g.P) return;
-  if (tiles[i] == 0) return;  // never gathered by the render passes
-  float T2[10];
-  chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[3 * i + 2].z), T2);
-  trec[3 * i + 0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
-  trec[3 * i + 1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
-  trec[3 * i + 2] = make_float4(T2[8], T2[9], 0.f, 0.f);
-}
 
 struct JvpPix {
   float T, dT, dC[3], dD;
@@ -276,42 +213,6 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
 }
 
 // ------------------------------------------------------------------ launchers
-int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
-                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s) {
-  if (g.P == 0) {
-    if (xp && xp->tail_p) {
-      set_error("internal: fused xpby with P = 0");
-      return GSLM_ERR_INVALID;
-    }
-    return GSLM_OK;
-  }
-  const unsigned nb = (unsigned)((g.P + 255) / 256);
-  XpbyK none{};
-  const XpbyK& x = xp ? *xp : none;
-  if (xp) {
-    if (t.rest && (t.rest != xp->p[2] || t.rest_stride != xp->w[2])) {
-      set_error("internal: fused xpby expects the tangent's SH-rest group to be p's");
-      return GSLM_ERR_INVALID;
-    }
-    const size_t lds = (size_t)256 * xp->w[2] * sizeof(float);
-    if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
-    else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
-  } else {
-    if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
-    else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
-  }
-  GSLM_LAUNCH_CHECK();
-  return GSLM_OK;
-}
-
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s) {
