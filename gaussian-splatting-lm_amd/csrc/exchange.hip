@@ -100,7 +100,7 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
   ViewsK vs;
   for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
   vs.n = nviews;
-  const size_t lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float) + 16;
+  const size_t lds = sh_stage_floats<false>(g.M) * sizeof(float) + 16;
   hipLaunchKernelGGL(k_gather_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, vs, g,
                      reinterpret_cast<const float4*>(screen), o);
   GSLM_LAUNCH_CHECK();

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
                                                          const uint32_t* __restrict__ tiles,
                                                          const uint32_t* __restrict__ goff,
                                                          const float4* __restrict__ rows, GradK out, int want_means) {
-  extern __shared__ __attribute__((aligned(16))) float s_buf[];  // row chunks, then [256][3M] SH grads
+  extern __shared__ __attribute__((aligned(16))) float s_buf[];  // row chunks, then the factored SH stage
   const int tid = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + tid;
@@ -56,25 +56,27 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
     write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
   }
   if (!sh_out) return;  // block-uniform
-  const int R = 3 * v.M;
+  // factored staging (gslm_gather.hpp): dsh[k][ch] = shB[k] dres[ch]
+  float* s_d = s_buf + 256 * SHB_STRIDE;
   if (i < g.P) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k < v.M) {
+    for (int k = 0; k < 16; ++k) s_buf[tid * SHB_STRIDE + k] = co.shB[k];
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) s_buf[tid * R + 3 * k + ch] = k < nc ? co.dsh[k][ch] : 0.f;
-      }
+    for (int ch = 0; ch < 3; ++ch) s_d[tid * 4 + ch] = co.dres[ch];
   }
   __syncthreads();
   const int acc = out.accumulate;
-  for (int64_t e = tid; e < nvalid * R; e += blockDim.x) {
-    const int64_t ii = e / R;
-    const int r = (int)(e - ii * R), k = r / 3, ch = r - 3 * k;
+  const int R = 3 * v.M;
+  const float invR = 1.0f / (float)R;
+  for (int e = tid; e < (int)nvalid * R; e += blockDim.x) {
+    const int ii = (int)(((float)e + 0.5f) * invR);  // exact: e < 256 R (see lm_epilogue)
+    const int r = e - ii * R, k = r / 3, ch = r - 3 * k;
+    const float val = k < nc ? s_buf[ii * SHB_STRIDE + k] * s_d[ii * 4 + ch] : 0.f;
     const int64_t gi = i0 + ii;
     if (k == 0) {
-      if (out.dc) put(&out.dc[gi * out.dc_stride + ch], s_buf[e], acc);
+      if (out.dc) put(&out.dc[gi * out.dc_stride + ch], val, acc);
     } else if (out.rest) {
-      put(&out.rest[gi * out.rest_stride + 3 * (k - 1) + ch], s_buf[e], acc);
+      put(&out.rest[gi * out.rest_stride + 3 * (k - 1) + ch], val, acc);
     }
   }
 }
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
                                                     const float4* __restrict__ rows, FlatK o) {
-  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(K-1)], first the row chunks
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // row chunks, then the factored SH stage
   __shared__ double s_dot[4];
   const int tid = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
   }
   ChainOut co;
   if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, WANT_MEANS, co);
-  lm_epilogue<WANT_MEANS>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
+  lm_epilogue<WANT_MEANS, true>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -108,7 +110,7 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
   (void)bb;
   if (g.P == 0) return GSLM_OK;
   const unsigned nb = (unsigned)((g.P + 255) / 256);
-  const size_t sh_lds = (size_t)256 * 3 * g.M * sizeof(float);
+  const size_t sh_lds = sh_stage_floats<true>(g.M) * sizeof(float);
   const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
   const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
   if (g.raw)
@@ -129,7 +131,7 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
   const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o);
   if (st) return st;
   const unsigned nb = (unsigned)((g.P + 255) / 256);
-  const size_t rest_lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float);
+  const size_t rest_lds = sh_stage_floats<true>(g.M) * sizeof(float);
   const size_t chunk_lds = (size_t)GATHER_CHUNK * (mask_xyz ? 2 : 3) * sizeof(float4);
   const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
   if (mask_xyz)

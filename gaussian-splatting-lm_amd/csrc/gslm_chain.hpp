@@ -101,6 +101,10 @@ struct ChainOut {
   float dcov[6];
   float dsh[16][3];
   float dcol[3];
+  // the SH gradient in factored form, dsh[k][ch] = shB[k] * dres[ch] (k < active coefficients): the
+  // per-Gaussian epilogues stage these 19 floats instead of the 3M products
+  float shB[16];
+  float dres[3];
 };
 
 // Reverse mode: G2 = reduced screen-space gradient [x_pix, y_pix, conic a, b, c, opacity_eff, r, g, b, invdepth].
@@ -116,7 +120,10 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
 #pragma unroll
   for (int k = 0; k < 6; ++k) co.dcov[k] = 0.f;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) co.dsh[k][0] = co.dsh[k][1] = co.dsh[k][2] = 0.f;
+  for (int k = 0; k < 16; ++k) {
+    co.dsh[k][0] = co.dsh[k][1] = co.dsh[k][2] = 0.f;
+    co.shB[k] = 0.f;
+  }
   if (!visible) return;
   Geo e;
   compute_geo<RAW>(v, g, i, clamped, e);
@@ -208,13 +215,17 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
     sh_basis(v.D, e.dir[0], e.dir[1], e.dir[2], B);
     const int nc = (v.D + 1) * (v.D + 1);
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
+    for (int k = 0; k < 16; ++k) {
+      co.shB[k] = k < nc ? B[k] : 0.f;
       if (k < nc) {
         co.dsh[k][0] = B[k] * dres[0];
         co.dsh[k][1] = B[k] * dres[1];
         co.dsh[k][2] = B[k] * dres[2];
       }
+    }
   }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) co.dres[ch] = dres[ch];
 
   if (want_means) {
     // J (EWA) dependence on the view-space mean

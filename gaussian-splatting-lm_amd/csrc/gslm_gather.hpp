@@ -94,10 +94,21 @@ inline int make_flatk(const GaussK& g, const GradK& y, const GradK& vin, const d
   return GSLM_OK;
 }
 
+// LDS staging of a block's SH gradients.  FACTORED (one view's chain): dsh[k][ch] = shB[k] dres[ch],
+// so 16 + 4 floats per Gaussian are staged (rows padded to 17 floats: conflict-free stores) and the
+// products are formed in the coalesced store loop -- 21 KB of LDS for 256 Gaussians instead of 46 KB,
+// which is the difference between 7 and 3 resident blocks per CU.  Otherwise (sums over views) the
+// 3(M-1) products themselves are staged.
+constexpr int SHB_STRIDE = 17;
+template <bool FACTORED>
+__host__ __device__ constexpr size_t sh_stage_floats(int M) {
+  return FACTORED ? (size_t)256 * (SHB_STRIDE + 4) : (size_t)256 * 3 * (M > 1 ? M - 1 : 0);
+}
+
 // Writes one block's 256 Gaussians' share of y (groups xyz, dc, rest, scaling, rotation, opacity)
 // from their ChainOut: y = (overwrite ? 0 : y) + J^T... + d v, and the block's partial of <v, y>.
-// Called by all 256 threads; co is ignored for threads past P.  s_rest: [256 * 3(M-1)] floats.
-template <bool WANT_MEANS>
+// Called by all 256 threads; co is ignored for threads past P.  s_rest: sh_stage_floats<FACTORED>(M).
+template <bool WANT_MEANS, bool FACTORED = false>
 __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const ChainOut& co, const FlatK& o, float* s_rest,
                                             double* s_dot) {
   const int tid = threadIdx.x;
@@ -131,17 +142,26 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
     dacc += store_group<4>(o.y[4], o.damp[4], u, 4 * i, ow, dot, co.drot, vr, yr);
     const float dop[1] = {co.dop};
     dacc += store_group<1>(o.y[5], o.damp[5], u, i, ow, dot, dop, vo, yo);
+    if (FACTORED) {
 #pragma unroll
-    for (int k = 1; k < 16; ++k)
-      if (k < g.M) {
+      for (int k = 0; k < 16; ++k) s_rest[tid * SHB_STRIDE + k] = co.shB[k];
+      float* s_d = s_rest + 256 * SHB_STRIDE;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) s_rest[tid * R + 3 * (k - 1) + ch] = k < nc ? co.dsh[k][ch] : 0.f;
-      }
+      for (int ch = 0; ch < 3; ++ch) s_d[tid * 4 + ch] = co.dres[ch];
+    } else {
+#pragma unroll
+      for (int k = 1; k < 16; ++k)
+        if (k < g.M) {
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) s_rest[tid * R + 3 * (k - 1) + ch] = k < nc ? co.dsh[k][ch] : 0.f;
+        }
+    }
   }
   __syncthreads();
   // coalesced store of the block's contiguous [nvalid * R] slice of the SH-rest group, 8 elements per
   // thread per step with all loads issued before any store
   const int64_t base = i0 * R, total = nvalid * R;
+  const float invR = R ? 1.0f / (float)R : 0.f;
   constexpr int U = 8;
   for (int64_t e0 = 0; e0 < total; e0 += (int64_t)U * blockDim.x) {
     float vin[U], yold[U];
@@ -156,7 +176,17 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
     for (int k = 0; k < U; ++k) {
       const int64_t e = e0 + (int64_t)k * blockDim.x + tid;
       if (e < total) {
-        float val = s_rest[e];
+        float val;
+        if (FACTORED) {
+          // e -> (Gaussian ii, coefficient k >= 1, channel ch); float quotient is exact here:
+          // e < 256 R, so (e + 0.5) / R stays >= 0.5 / R away from every integer
+          const int ii = (int)(((float)e + 0.5f) * invR);
+          const int r = (int)e - ii * R;
+          const int k = 1 + r / 3, ch = r - 3 * (k - 1);
+          val = k < nc ? s_rest[ii * SHB_STRIDE + k] * s_rest[256 * SHB_STRIDE + ii * 4 + ch] : 0.f;
+        } else {
+          val = s_rest[e];
+        }
         if (u) val += o.damp[2] * vin[k];
         const float out = ow ? val : yold[k] + val;
         o.y[2][base + e] = out;
