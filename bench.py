@@ -207,6 +207,10 @@ def main():
     # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
     fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
 
+    # ---------------- BASELINE configs[2] as train_jvp.py runs it: one full LM step (loss, J^T b, CGLS with
+    # 10 iterations and the reference's residual monitor, 7-point line search on the validation view)
+    lm = time_lm_step(model, cams, bg) if world_size == 1 else None
+
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -249,11 +253,28 @@ def main():
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms},
             "cpu_baseline": cpu,
             "raster_fwd_bwd": fb,
+            "lm_step": lm,
         }
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_lm_step(model, cams, bg, iters=10, reps=2):
+    """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = restart_iter = iters and check_every=True
+    (host-side stopping tests each iteration, as the reference's CGLS); validation view = the batch."""
+    from gslm.lm import lm_step
+    lm_step(model, cams, cams, bg, max_iter=iters, restart_iter=iters, check_every=True)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = lm_step(model, cams, cams, bg, max_iter=iters, restart_iter=iters, check_every=True)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    return {"config": f"full LM step, {len(cams)} view(s), CGLS {iters} iterations + 7-point line search "
+                      "(BASELINE configs[2])", "ms": 1e3 * t, "cg_iters": out["cg"]["iters"],
+            "loss_start": out["start_loss"], "loss_final": out["final_val_loss"]}
 
 
 def time_drop_in_fwd_bwd(device, W, H, s0, P=100_000, sh=3, reps=10):

@@ -114,6 +114,11 @@ EXPORTS = {
     "gslm_damp_add": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                      ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p]),
+    "gslm_residual_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "gslm_lm_residual": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32,
+                                        ctypes.c_void_p]),
     "gslm_inspect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -95,20 +95,36 @@ class LMProblem:
                                        dtype=torch.float64, device=device)
         self.weights = [None] * len(cams)
         self.residuals = [None] * len(cams)
+        self.seeds = [None] * len(cams)
+        self.res_scratch = torch.empty(lib.gslm_residual_scratch_bytes(1, 1) // 8, dtype=torch.float64,
+                                       device=device)
 
     # -------------------------------------------------------------- residual (A8)
     def evaluate(self):
-        """Primal forward of every view; residuals, per-pixel weights, loss = 2 sum ||r||^2 (device)."""
+        """Primal forward of every view; residuals, per-pixel weights and the J^T b seeds from one fused
+        epilogue per view (gslm_lm_residual); loss = 2 sum ||r||^2 (device double)."""
         g = raw_gaussians(self.model)
         loss = torch.zeros((), dtype=torch.float64, device=self.device)
         for b, vr in enumerate(self.views):
             R = vr.forward(g, self.stream)
+            if self.residuals[b] is None or self.residuals[b].shape != R.shape:
+                self.residuals[b] = torch.empty_like(R)
+                self.weights[b] = torch.empty_like(R)
+                self.seeds[b] = torch.empty_like(R)
             m = self.masks[b]
-            inside = ((R >= 0) & (R <= 1)).to(torch.float32)
-            r = m * R.clamp(0, 1) - self.gts[b]
-            self.residuals[b] = r
-            self.weights[b] = (m * m * inside).contiguous()
-            loss += 2.0 * (r.double() * r.double()).sum()
+            gt = self.gts[b]
+            if m is not None:
+                m = m.to(torch.float32).contiguous()
+                if m.numel() != vr.H * vr.W:
+                    raise ValueError("alpha mask must be [1, H, W]")
+            if gt.shape != R.shape or gt.dtype != torch.float32:
+                raise ValueError(f"ground truth must be float32 {tuple(R.shape)}, got {gt.dtype} {tuple(gt.shape)}")
+            gt = gt.contiguous()
+            check(lib.gslm_lm_residual(vr.H, vr.W, R.data_ptr(), gt.data_ptr(), None if m is None else m.data_ptr(),
+                                       self.residuals[b].data_ptr(), self.weights[b].data_ptr(),
+                                       self.seeds[b].data_ptr(), self.res_scratch.data_ptr(),
+                                       self.res_scratch.numel() * 8, loss.data_ptr(), int(b > 0), self.stream),
+                  "gslm_lm_residual")
         self.loss = loss
         return loss
 
@@ -122,10 +138,7 @@ class LMProblem:
         g = raw_gaussians(self.model)
         grads = self.layout.grads_struct(out, accumulate=True)
         for b, vr in enumerate(self.views):
-            m = self.masks[b]
-            R = vr.color
-            inside = ((R >= 0) & (R <= 1)).to(torch.float32)
-            dL = (-2.0 * m * inside * self.residuals[b]).contiguous()
+            dL = self.seeds[b]  # -2 m 1[0 <= R <= 1] r, from gslm_lm_residual
             check(lib.gslm_backward(ctypes.byref(vr.view), ctypes.byref(g), vr.geom.data_ptr(), vr.binning.data_ptr(),
                                     vr.N, vr.image.data_ptr(), dL.data_ptr(), None, vr.scratch.data_ptr(),
                                     vr.scratch.numel(), ctypes.byref(grads), self.stream), "gslm_backward")

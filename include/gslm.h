@@ -226,6 +226,20 @@ int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* s
 int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const double* group_damp,
                   int32_t ngroups, float* y, void* stream);
 
+/* ---- LM residual epilogue of one view (replaces the render clamp
+ * gaussian_renderer/batch_render.py:118 + compute_batch_loss_block, solver/batch_training_loss.py:10-17,
+ * 56-67, disable_ssim=True, and loss_scalar, solver/loss_image_state.py:16-19) ----
+ * color / gt / residual / weight / seed are [3,H,W]; alpha_mask [H,W] or NULL (= 1).  Writes
+ *   residual = m clamp(color, 0, 1) - gt          (NULL: not written)
+ *   weight   = m^2 1[0 <= color <= 1]             (the per-pixel weight of gslm_matvec_view_ex)
+ *   seed     = -2 m 1[0 <= color <= 1] residual   (NULL: not written; gslm_backward's dL/dcolor for J^T b)
+ * and *loss_dev (device double) = [*loss_dev if accumulate] + 2 sum residual^2 ([r; r] aliasing).
+ * Deterministic (fixed two-pass reduction); scratch >= gslm_residual_scratch_bytes(H, W). */
+size_t gslm_residual_scratch_bytes(int32_t H, int32_t W);
+int gslm_lm_residual(int32_t H, int32_t W, const float* color, const float* gt, const float* alpha_mask,
+                     float* residual, float* weight, float* seed, void* scratch, size_t scratch_bytes,
+                     double* loss_dev, int32_t accumulate, void* stream);
+
 /* ---- diagnostics: device-to-device copies of internal buffers (any output may be NULL) ----
  * point_list [N] u32 (Gaussian id per sorted slot), ranges [ntiles*2] u32, tiles_touched [P] u32,
  * final_T [H*W] f32, n_contrib [H*W] u32, render records [P*12] f32. */

@@ -173,3 +173,32 @@ def test_tail_rows_written_once_per_geometry():
     assert not any(vr.tail_clean for vr in prob.views)
     y3 = prob.matvec(v, prob.zeros())
     assert torch.equal(y1, ref) and torch.equal(y2, ref) and torch.equal(y3, ref)
+
+
+@pytest.mark.parametrize("with_mask", [False, True])
+def test_fused_residual_matches_reference_formulas(with_mask):
+    """gslm_lm_residual against the reference's torch expressions (batch_render.py:118 clamp,
+    batch_training_loss.py:10-17 / 56-67, loss_image_state.py:16-19): r, weight and the J^T b seed
+    bit-identical, loss = 2 ||r||^2 to 1e-12, on renders with values outside [0, 1]."""
+    from gslm import _lib
+    H, W = 37, 53
+    g = torch.Generator().manual_seed(11)
+    R = (torch.rand(3, H, W, generator=g) * 2.0 - 0.5).cuda()
+    gt = torch.rand(3, H, W, generator=g).cuda()
+    m = torch.rand(1, H, W, generator=g).cuda() if with_mask else None
+    res, w, seed = (torch.empty_like(R) for _ in range(3))
+    loss = torch.full((), 5.0, dtype=torch.float64, device="cuda")
+    scratch = torch.empty(_lib.lib.gslm_residual_scratch_bytes(H, W) // 8, dtype=torch.float64, device="cuda")
+    for acc in (0, 1):
+        _lib.check(_lib.lib.gslm_lm_residual(H, W, R.data_ptr(), gt.data_ptr(), None if m is None else m.data_ptr(),
+                                             res.data_ptr(), w.data_ptr(), seed.data_ptr(), scratch.data_ptr(),
+                                             scratch.numel() * 8, loss.data_ptr(), acc, _lib.stream_handle()))
+    torch.cuda.synchronize()
+    mm = torch.ones(1, H, W, device="cuda") if m is None else m
+    inside = ((R >= 0) & (R <= 1)).to(torch.float32)
+    r_ref = mm * R.clamp(0, 1) - gt
+    assert torch.equal(res, r_ref)
+    assert torch.equal(w, mm * mm * inside)
+    assert torch.equal(seed, -2.0 * mm * inside * r_ref)
+    ref_loss = 2.0 * 2.0 * (r_ref.double() ** 2).sum().item()  # written once, then accumulated once
+    assert abs(loss.item() - ref_loss) <= 1e-12 * ref_loss
