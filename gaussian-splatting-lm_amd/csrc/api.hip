@@ -371,10 +371,19 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
     xp.tail_n = opts->xpby_tail_n;
     if (xp.tail_p && !xp.tail_s) { set_error("matvec: xpby tail without s"); return GSLM_ERR_INVALID; }
   }
+  const float* seed = opts ? opts->pixel_seed : nullptr;
+  if (seed && (!mask_xyz || fused_xpby || (stages & (GSLM_STAGE_TANGENT | GSLM_STAGE_SCREEN)))) {
+    set_error("matvec: pixel_seed (J^T seed) needs mask_xyz and excludes TANGENT / SCREEN / xpby");
+    return GSLM_ERR_INVALID;
+  }
   if ((stages & GSLM_STAGE_TANGENT) &&
       (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s)))
     return st;
-  if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
+  if (seed) {
+    if ((stages & GSLM_STAGE_RENDER) &&
+        (st = launch_render_vjp_lm(b.v, b.gb, b.bb, b.ib, N, seed, b.sb, opts->flags & GSLM_MV_TAIL_CLEAN, s)))
+      return st;
+  } else if ((stages & GSLM_STAGE_RENDER) && N > 0 &&
       (st = launch_matvec_render(b.v, t, b.gb, b.bb, b.ib, b.sb, N, pixel_weight, mask_xyz != 0,
                                  opts && (opts->flags & GSLM_MV_TAIL_CLEAN), s)))
     return st;

@@ -12,7 +12,9 @@
 
 namespace gslm {
 
-template <bool WITH_XY, bool WITH_INV>
+// ROWF4 = 3: drop-in rows (screen position and inverse depth too); ROWF4 = 2: the LM rows of
+// k_render_matvec (xyz frozen, no depth term), which k_gather_lm consumes -- the J^T b of an LM step.
+template <bool WITH_XY, bool WITH_INV, int ROWF4>
 __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
@@ -22,7 +24,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
                                                      const float* __restrict__ final_T,
                                                      const uint32_t* __restrict__ n_contrib,
                                                      const float* __restrict__ dL_dcolor,
-                                                     const float* __restrict__ dL_dinv, float4* __restrict__ rows) {
+                                                     const float* __restrict__ dL_dinv, float4* __restrict__ rows,
+                                                     int write_tail) {
   // 128-entry batches (as k_render_matvec): 24-26 KB of LDS per block -> 6 blocks per CU
   constexpr int B = 128;
   __shared__ float4 s_r0[B], s_r1[B];
@@ -50,8 +53,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __rest
   }
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, d0, d1, d2, di);
-  vjp_tile<WITH_XY, WITH_INV, 3, B>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list, rec,
-                                 slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows, true);
+  vjp_tile<WITH_XY, WITH_INV, ROWF4, B>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list,
+                                     rec, slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows,
+                                     write_tail != 0);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -60,11 +64,28 @@ int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
   const int ntiles = v.gx * v.gy;
   if (N == 0) return GSLM_OK;
   if (dL_dinv)
-    hipLaunchKernelGGL((k_render_bwd<true, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
+    hipLaunchKernelGGL((k_render_bwd<true, true, 3>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv,
+                       sb.contrib, 1);
   else
-    hipLaunchKernelGGL((k_render_bwd<true, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                       gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv, sb.contrib);
+    hipLaunchKernelGGL((k_render_bwd<true, false, 3>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv,
+                       sb.contrib, 1);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_render_vjp_lm(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, int64_t N,
+                         const float* dL_dcolor, const ScratchBufs& sb, bool tail_clean, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (N == 0) return GSLM_OK;
+  if (!tail_clean) {  // slots and tail rows: once per geometry, shared with k_render_matvec
+    const int st = launch_row_slots(v, gb, bb, N, s);
+    if (st) return st;
+  }
+  hipLaunchKernelGGL((k_render_bwd<false, false, 2>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                     bb.point_list, gb.rec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, nullptr,
+                     sb.contrib, tail_clean ? 0 : 1);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

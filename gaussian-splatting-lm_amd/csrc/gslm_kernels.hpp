@@ -351,6 +351,8 @@ int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
 namespace gslm {
 int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, int64_t N,
                       const float* dL_dcolor, const float* dL_dinv, const ScratchBufs& sb, hipStream_t s);
+int launch_render_vjp_lm(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, int64_t N,
+                         const float* dL_dcolor, const ScratchBufs& sb, bool tail_clean, hipStream_t s);
 int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, const BinBufs& bb,
                           const ScratchBufs& sb, const GradK& out, bool want_means, hipStream_t s);
 // Fused CG direction update run by the tangent kernel before it reads the direction: every

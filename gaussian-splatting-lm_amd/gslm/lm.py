@@ -132,10 +132,31 @@ class LMProblem:
         return [v.N for v in self.views]
 
     # -------------------------------------------------------------- J^T b
-    def rhs(self, out):
-        """out = J^T b = -2 sum_b J_b^T (m (.) 1[0<=R<=1] (.) r_b) in the flat layout (xyz, exposure zeroed)."""
-        out.zero_()
+    def rhs(self, out, fused=True):
+        """out = J^T b = -2 sum_b J_b^T (m (.) 1[0<=R<=1] (.) r_b) in the flat layout (xyz, exposure zeroed).
+
+        fused: the LM path -- a back-to-front pass seeded with gslm_lm_residual's seed into the LM
+        rows, then the LM gather (gslm_matvec_view_ex with pixel_seed); otherwise the drop-in
+        gslm_backward (general rows, every parameter group)."""
         g = raw_gaussians(self.model)
+        if fused and self.mask_xyz:
+            ys = self.layout.grads_struct(out)
+            for b, vr in enumerate(self.views):
+                opts = _lib.GslmMatvecOpts()
+                opts.stages = 2 | 4 | (STAGE_OVERWRITE if b == 0 else 0)  # RENDER | GATHER
+                opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
+                opts.pixel_seed = self.seeds[b].data_ptr()
+                check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(ys),
+                                              self.seeds[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                              vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                              ctypes.byref(ys), ctypes.byref(opts), self.stream), "gslm_matvec_view_ex")
+                vr.tail_clean = True
+            if not self.views:
+                out.zero_()
+            e0, e1 = self.layout.offsets["exposure"]
+            out[e0:e1].zero_()
+            return out
+        out.zero_()
         grads = self.layout.grads_struct(out, accumulate=True)
         for b, vr in enumerate(self.views):
             dL = self.seeds[b]  # -2 m 1[0 <= R <= 1] r, from gslm_lm_residual

@@ -185,6 +185,11 @@ typedef struct gslm_matvec_opts {
   const float* xpby_tail_s;
   int64_t xpby_tail_n;
   float* screen_out;      /* GSLM_STAGE_SCREEN output, P x 8 floats */
+  /* J^T seed instead of J^T W J v: when set, RENDER runs only the back-to-front pass with dL/dcolor =
+   * pixel_seed ([3,H,W], e.g. gslm_lm_residual's seed) into the LM rows, and GATHER sums them as usual
+   * (v is then only read for D v / dot_vy).  Needs mask_xyz; excludes TANGENT, SCREEN and xpby.  This
+   * is the J^T b of an LM step (train_jvp.py:243, solver_functions.py:101-132) on the fused path. */
+  const float* pixel_seed;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,

@@ -154,8 +154,8 @@ def test_fused_xpby_matches_separate():
 def test_tail_rows_written_once_per_geometry():
     """GSLM_MV_TAIL_CLEAN: the zero rows of never-blended entries are written by the first product on a
     geometry and skipped afterwards.  A scratch poisoned with NaN before the first product, a second
-    product reusing the tail, and a product after rhs() (whose backward reuses the scratch with
-    48-byte rows) must all equal a fresh problem's product bitwise."""
+    product reusing the tail, and a product after the drop-in rhs (whose backward reuses the scratch
+    with 48-byte rows) must all equal a fresh problem's product bitwise."""
     from gslm.lm import LMProblem
     d, m, cams = _load()
     v = torch.from_numpy(d["v"]).cuda()
@@ -169,7 +169,7 @@ def test_tail_rows_written_once_per_geometry():
     y1 = prob.matvec(v, prob.zeros()).clone()
     assert all(vr.tail_clean for vr in prob.views)
     y2 = prob.matvec(v, prob.zeros()).clone()
-    prob.rhs(prob.zeros())
+    prob.rhs(prob.zeros(), fused=False)  # the drop-in backward's 48-byte rows overwrite the scratch
     assert not any(vr.tail_clean for vr in prob.views)
     y3 = prob.matvec(v, prob.zeros())
     assert torch.equal(y1, ref) and torch.equal(y2, ref) and torch.equal(y3, ref)
@@ -202,3 +202,22 @@ def test_fused_residual_matches_reference_formulas(with_mask):
     assert torch.equal(seed, -2.0 * mm * inside * r_ref)
     ref_loss = 2.0 * 2.0 * (r_ref.double() ** 2).sum().item()  # written once, then accumulated once
     assert abs(loss.item() - ref_loss) <= 1e-12 * ref_loss
+
+
+def test_fused_rhs_matches_dropin_backward():
+    """J^T b on the LM path (seeded back-to-front pass into LM rows + LM gather) equals the drop-in
+    gslm_backward's (general rows), up to summation order; then the matvec reusing the tail rows the
+    fused rhs wrote matches a fresh problem's product bitwise."""
+    from gslm.lm import LMProblem
+    d, m, cams = _load()
+    prob = LMProblem(m, cams, torch.zeros(3))
+    prob.evaluate()
+    g_fused = prob.rhs(prob.zeros()).clone()
+    assert all(vr.tail_clean for vr in prob.views)
+    v = torch.from_numpy(d["v"]).cuda()
+    y = prob.matvec(v, prob.zeros()).clone()
+    g_drop = prob.rhs(prob.zeros(), fused=False)
+    assert _close(g_fused.cpu().numpy(), g_drop.cpu().numpy(), 1e-5)
+    fresh = LMProblem(m, cams, torch.zeros(3))
+    fresh.evaluate()
+    assert torch.equal(y, fresh.matvec(v, fresh.zeros()))
