@@ -91,37 +91,61 @@ __global__ __launch_bounds__(256) void k_xpby_dev(int64_t n, const float* __rest
 
 // One CG step on flat vectors, a = gam / del (device scalars):
 //   x += a p ;  s -= a q ;  part[block] = sum s_new^2     (then k_dot_final -> gamma')
+// MONITOR also accumulates <x_new, g> and <x_new, s_new> (partials at part + nb, part + 2 nb): the
+// residual monitor of conjugate_gradient.py:103-104, b^2 - <x, J^T b> - <x, s>, without two more
+// passes over x.
+template <bool MONITOR>
 __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const double* __restrict__ gam,
                                                            const double* __restrict__ del,
                                                            const float* __restrict__ p, const float* __restrict__ q,
                                                            float* __restrict__ x, float* __restrict__ s,
-                                                           double* __restrict__ part) {
+                                                           const float* __restrict__ g, double* __restrict__ part) {
   __shared__ double sm[DOT_THREADS / 64];
   const float a = (float)((*gam) / (*del));
-  double acc = 0.0;
+  double acc = 0.0, axg = 0.0, axs = 0.0;
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * DOT_THREADS;
   const float4* p4 = reinterpret_cast<const float4*>(p);
   const float4* q4 = reinterpret_cast<const float4*>(q);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
   float4* x4 = reinterpret_cast<float4*>(x);
   float4* s4 = reinterpret_cast<float4*>(s);
   for (int64_t i = (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n4; i += stride) {
     const float4 pv = p4[i], qv = q4[i];
     float4 xv = x4[i], sv = s4[i];
+    float4 gv;
+    if (MONITOR) gv = g4[i];
     xv.x += a * pv.x; xv.y += a * pv.y; xv.z += a * pv.z; xv.w += a * pv.w;
     sv.x -= a * qv.x; sv.y -= a * qv.y; sv.z -= a * qv.z; sv.w -= a * qv.w;
     x4[i] = xv;
     s4[i] = sv;
     acc += (double)sv.x * sv.x + (double)sv.y * sv.y + (double)sv.z * sv.z + (double)sv.w * sv.w;
+    if (MONITOR) {
+      axg += (double)xv.x * gv.x + (double)xv.y * gv.y + (double)xv.z * gv.z + (double)xv.w * gv.w;
+      axs += (double)xv.x * sv.x + (double)xv.y * sv.y + (double)xv.z * sv.z + (double)xv.w * sv.w;
+    }
   }
   for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n; i += stride) {
-    x[i] += a * p[i];
+    const float xv = x[i] + a * p[i];
+    x[i] = xv;
     const float sv = s[i] - a * q[i];
     s[i] = sv;
     acc += (double)sv * sv;
+    if (MONITOR) {
+      axg += (double)xv * g[i];
+      axs += (double)xv * sv;
+    }
   }
   const double t = block_sum_d(acc, sm);
   if (threadIdx.x == 0) part[blockIdx.x] = t;
+  if (MONITOR) {
+    __syncthreads();
+    const double t1 = block_sum_d(axg, sm);
+    if (threadIdx.x == 0) part[gridDim.x + blockIdx.x] = t1;
+    __syncthreads();
+    const double t2 = block_sum_d(axs, sm);
+    if (threadIdx.x == 0) part[2 * gridDim.x + blockIdx.x] = t2;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_damp_add(int64_t n, const float* __restrict__ x, Groups g,
@@ -168,9 +192,32 @@ int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, cons
     return GSLM_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_cg_update, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s,
-                     (double*)scratch);
+  hipLaunchKernelGGL(k_cg_update<false>, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s,
+                     nullptr, (double*)scratch);
   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, (const double*)scratch, DOT_BLOCKS, gam_new_dev);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
+                           float* x, float* s, const float* g, void* scratch, size_t scratch_bytes,
+                           double* gam_new_dev, double* xg_dev, double* xs_dev, void* stream) {
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(x) |
+       reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(g)) & 15) {
+    set_error("gslm_cg_update_monitor: vectors must be 16-byte aligned");
+    return GSLM_ERR_INVALID;
+  }
+  if (scratch_bytes < (size_t)3 * DOT_BLOCKS * sizeof(double)) {
+    set_error("gslm_cg_update_monitor: scratch < 3 * 1024 doubles");
+    return GSLM_ERR_CAPACITY;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const double* part = (const double*)scratch;
+  hipLaunchKernelGGL(k_cg_update<true>, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s, g,
+                     (double*)scratch);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part, DOT_BLOCKS, gam_new_dev);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + DOT_BLOCKS, DOT_BLOCKS, xg_dev);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + 2 * DOT_BLOCKS, DOT_BLOCKS, xs_dev);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -91,7 +91,8 @@ class LMProblem:
         self.masks = [c.alpha_mask.to(device) for c in cams] if alpha_masks is None else alpha_masks
         self.views = [ViewRaster(_lib.view_from_camera(c, bg, model.active_sh_degree), device) for c in cams]
         self.stream = _lib.stream_handle(device)
-        self.dot_scratch = torch.empty(lib.gslm_dot_scratch_bytes(max(P, self.layout.numel)) // 8 + 8,
+        # >= 3 x 1024 doubles: gslm_cg_update_monitor's three partial sums
+        self.dot_scratch = torch.empty(max(lib.gslm_dot_scratch_bytes(max(P, self.layout.numel)) // 8, 3 * 1024) + 8,
                                        dtype=torch.float64, device=device)
         self.weights = [None] * len(cams)
         self.residuals = [None] * len(cams)
@@ -354,14 +355,17 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                     print("Early termination: delta is too small.")
                 stop = True
                 break
-            # x += alpha p ; s -= alpha q ; gamma' = <s, s>   (one pass)
-            check(lib.gslm_cg_update(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(), s.data_ptr(),
-                                     prob.dot_scratch.data_ptr(), ptr(GAMN), st))
+            # x += alpha p ; s -= alpha q ; gamma' = <s, s> [; <x, g>, <x, s> for the monitor]  (one pass)
+            if check_every:
+                check(lib.gslm_cg_update_monitor(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(),
+                                                 s.data_ptr(), g.data_ptr(), prob.dot_scratch.data_ptr(),
+                                                 prob.dot_scratch.numel() * 8, ptr(GAMN), ptr(XG), ptr(XS), st))
+            else:
+                check(lib.gslm_cg_update(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(),
+                                         s.data_ptr(), prob.dot_scratch.data_ptr(), ptr(GAMN), st))
             # beta = gamma' / gamma; after the slot swap below these are the GAM / GAMN slots
             pre = (s, ptr(GAMN), ptr(GAM))
             if check_every:
-                prob.dot(x, g, ptr(XG))
-                prob.dot(x, s, ptr(XS))
                 vals = sc[:5].tolist()
                 res = b2 - vals[XG] - vals[XS]  # ||b - J x||^2 + x^T D x  (monitor of conjugate_gradient.py:103-104)
                 history.append(res)

@@ -225,6 +225,11 @@ int gslm_xpby_dev(int64_t n, const float* s, const double* num_dev, const double
  * *gam_new_dev = <s, s> (scratch >= gslm_dot_scratch_bytes(n)).  Vectors 16-byte aligned. */
 int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                    float* x, float* s, void* scratch, double* gam_new_dev, void* stream);
+/* gslm_cg_update plus the residual monitor of conjugate_gradient.py:103-104 in the same pass:
+ * *xg_dev = <x_new, g>, *xs_dev = <x_new, s_new> (g = J^T b).  scratch >= 3 * 1024 doubles. */
+int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
+                           float* x, float* s, const float* g, void* scratch, size_t scratch_bytes,
+                           double* gam_new_dev, double* xg_dev, double* xs_dev, void* stream);
 /* *out_dev = sum of np per-block partials (second pass of the fused dots) */
 int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* stream);
 /* y += d[group] * x (the damping term D x) */
