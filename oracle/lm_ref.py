@@ -6,7 +6,8 @@ vectors the reference's own solver produced (tests/golden/solver_golden.npz) and
 the HIP operator in multi-process (gloo) tests of the view sharding:
 
   residual        r_b = m_b * clamp01(R_b) - gt_b, residual vector [r; r]
-                  (batch_training_loss.py:10-17, disable_ssim=True)
+                  (batch_training_loss.py:10-17, disable_ssim=True); with ssim=True the vector is
+                  [r1; r2] of oracle/ssim_ref.py (batch_training_loss.py:18-30)
   J^T b           -2 sum_b J_r^T r_b                      (solver_functions.py:101-132 with b = -[r; r])
   (J^T J + D) v   2 sum_b J_r^T J_r v + D v               (matvec, matvec_T, GaussianModelDampMatrix)
   CGLS            conjugate_gradient.py:51-127 in its normal-equations form, float64 scalars
@@ -17,6 +18,7 @@ import torch
 import torch.autograd.forward_ad as fwAD
 
 from gslm.params import GROUPS, ParamLayout
+from oracle import ssim_ref
 from oracle import torch_raster as tr
 
 DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
@@ -24,9 +26,10 @@ DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling
 
 
 class OracleLMProblem:
-    def __init__(self, model, cams, bg, mask_xyz=True, damp=None):
+    def __init__(self, model, cams, bg, mask_xyz=True, damp=None, ssim=False, lambda_dssim=0.2):
         self.model, self.cams, self.bg = model, cams, bg
         self.mask_xyz = mask_xyz
+        self.ssim, self.lambda_dssim = ssim, lambda_dssim
         self.damp = DEFAULT_DAMP if damp is None else damp
         P = model._xyz.shape[0]
         K = 1 + model._features_rest.shape[1]
@@ -37,15 +40,24 @@ class OracleLMProblem:
         return [m._xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure]
 
     def _residuals(self):
+        """Residual blocks; each enters the loss and J^T J with factor self._fac (2: the [r; r] aliasing)."""
         out = []
         for c in self.cams:
             img, _, _, _ = tr.render_model(self.model, c, self.bg)
-            out.append(img * c.alpha_mask - c.original_image)
+            x = img * c.alpha_mask
+            if self.ssim:
+                out.extend(ssim_ref.ssim_residuals(x, c.original_image, self.lambda_dssim))
+            else:
+                out.append(x - c.original_image)
         return out
+
+    @property
+    def _fac(self):
+        return 1.0 if self.ssim else 2.0
 
     def evaluate(self):
         with torch.no_grad():
-            self.loss = sum(2.0 * (r.double() ** 2).sum() for r in self._residuals())
+            self.loss = sum(self._fac * (r.double() ** 2).sum() for r in self._residuals())
         return self.loss
 
     def _flatten(self, tensors):
@@ -62,7 +74,7 @@ class OracleLMProblem:
         leaves = self._leaves()
         for t in leaves:
             t.grad = None
-        loss = sum((r * r).sum() for r in self._residuals())
+        loss = sum((0.5 * self._fac) * (r * r).sum() for r in self._residuals())  # J^T b = -grad
         grads = torch.autograd.grad(loss, leaves, allow_unused=True)
         g = self._flatten([-(gr if gr is not None else torch.zeros_like(t)) for gr, t in zip(grads, leaves)])
         g = self._mask(g.detach())
@@ -83,7 +95,7 @@ class OracleLMProblem:
             finally:
                 (m._xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure) = saved
         return [t if t is not None else torch.zeros(3, c.image_height, c.image_width)
-                for t, c in zip(tangents, self.cams)]
+                for t, c in zip(tangents, [c for c in self.cams for _ in range(2 if self.ssim else 1)])]
 
     def damp_add(self, v, y):
         for gname in GROUPS:
@@ -97,7 +109,7 @@ class OracleLMProblem:
         jv = self._jr_v(v)
         leaves = self._leaves()
         res = self._residuals()
-        obj = sum((r * (2.0 * t.detach())).sum() for r, t in zip(res, jv))
+        obj = sum((r * (self._fac * t.detach())).sum() for r, t in zip(res, jv))
         grads = torch.autograd.grad(obj, leaves, allow_unused=True)
         out = self._flatten([gr if gr is not None else torch.zeros_like(t) for gr, t in zip(grads, leaves)])
         y.copy_(self._mask(out.detach()))

@@ -16,6 +16,11 @@ What is pinned by the *reference's code* (imported from /root/reference, never c
                        train_jvp.py:221-258 drives them (disable_ssim residual, xyz mask, damping):
                        loss, J^T b, (J^T J + D) v, and the CGLS solutions for the reference schedule
                        (max_iter=2, restart_iter=1) and for max_iter=restart_iter=10.
+  * ssim_golden.npz    utils/loss_utils.py ssim_per_pixel / l1_loss_per_pixel on random image pairs
+                       and on the solver scene's renders (the SSIM residual)
+  * solver_ssim_golden.npz  the same solver run with the disable_ssim=False residual
+                       (solver/batch_training_loss.py:18-30, restated around the reference's own
+                       l1_loss_per_pixel / ssim_per_pixel): loss, J^T b, (J^T J + D) v, 10-iteration CGLS
 The rasterizer itself has no reference binary here (absent submodule): its numerics are pinned by
 the oracle restatement, finite differences and the adjoint identity (tests/test_oracle.py).
 """
@@ -142,6 +147,87 @@ def oracle_batch_loss(gaussians, viewpoint_cams, batch_stats=None, BatchLossImag
     return BatchLossImageState(r, r, depth, sizes, False)
 
 
+def oracle_batch_loss_ssim(gaussians, viewpoint_cams, batch_stats=None, BatchLossImageState=None, ref=None,
+                           lambda_dssim=0.2):
+    """batch_training_loss(disable_ssim=False, FUSED_SSIM_AVAILABLE=False) (solver/batch_training_loss.py:
+    10-30, 56-81) on the oracle renderer, with the reference's l1_loss_per_pixel / ssim_per_pixel."""
+    l1_loss_per_pixel, ssim_per_pixel = ref
+    bg = torch.zeros(3)
+    images = torch.stack([tr.render_model(gaussians, vc, bg)[0] for vc in viewpoint_cams])
+    gt = torch.stack([vc.original_image for vc in viewpoint_cams])
+    masks = torch.stack([vc.alpha_mask for vc in viewpoint_cams])
+    images = images * masks
+    alphas, betas = [], []
+    for vc in viewpoint_cams:
+        n = 3 * int(vc.image_height) * int(vc.image_width)
+        alphas.append(math.sqrt((1.0 - lambda_dssim) / n))
+        betas.append(math.sqrt(lambda_dssim / n))
+    alphas = torch.tensor(alphas, dtype=images.dtype).view(-1, 1, 1, 1)
+    betas = torch.tensor(betas, dtype=images.dtype).view(-1, 1, 1, 1)
+    l1 = l1_loss_per_pixel(images, gt)
+    ssim_loss = (1.0 - ssim_per_pixel(images, gt)).abs()
+    r1 = alphas * torch.sqrt(l1 + 1e-6)
+    r2 = betas * torch.sqrt(ssim_loss + 1e-6)
+    depth = torch.zeros((0,), dtype=r1.dtype, requires_grad=True)
+    sizes = [(vc.image_height, vc.image_width) for vc in viewpoint_cams]
+    return BatchLossImageState(r1, r2, depth, sizes, False)
+
+
+def ssim_golden():
+    with reference_on_path():
+        from utils.loss_utils import l1_loss_per_pixel, ssim_per_pixel
+    g = torch.Generator().manual_seed(21)
+    out = {}
+    a = torch.rand(2, 3, 37, 53, generator=g)
+    b = (a + 0.1 * torch.randn(2, 3, 37, 53, generator=g)).clamp(0, 1)
+    out["rand_a"], out["rand_b"] = a.numpy(), b.numpy()
+    out["rand_ssim"] = ssim_per_pixel(a, b).numpy()
+    out["rand_l1"] = l1_loss_per_pixel(a, b).numpy()
+    model, cams = solver_scene()
+    imgs = torch.stack([tr.render_model(model, c, torch.zeros(3))[0].detach() for c in cams])
+    gts = torch.stack([c.original_image for c in cams])
+    out["scene_x"], out["scene_gt"] = imgs.numpy(), gts.numpy()
+    out["scene_ssim"] = ssim_per_pixel(imgs, gts).numpy()
+    np.savez_compressed(os.path.join(HERE, "ssim_golden.npz"), **out)
+
+
+def solver_ssim_golden():
+    with reference_on_path():
+        from solver.conjugate_gradient import cgls_damped
+        from solver.gaussian_model_state import (GaussianModelDampMatrix, GaussianModelParamGroupMask,
+                                                 GaussianModelState)
+        from solver.loss_image_state import BatchLossImageState
+        from solver.solver_functions import LinearSolverFunctions
+        from utils.loss_utils import l1_loss_per_pixel, ssim_per_pixel
+    model, cams = solver_scene()
+    loss_func = partial(oracle_batch_loss_ssim, BatchLossImageState=BatchLossImageState,
+                        ref=(l1_loss_per_pixel, ssim_per_pixel))
+    param_mask = GaussianModelParamGroupMask(mask_xyz=True)
+    damp = GaussianModelDampMatrix(xyz_damp=5e2, features_dc_damp=5e-2, features_rest_damp=5e-2, scaling_damp=5e-2,
+                                   rotation_damp=5e-2, opacity_damp=5e-2, exposure_damp=1e1)
+    out = {}
+    st = LinearSolverFunctions(loss_func, model, cams, batch_size=20, param_mask=param_mask)
+    out["loss"] = np.array(float(st.evaluate_loss().loss_scalar))
+    with torch.no_grad():
+        b = -1 * st.loss
+        out["Jtb"] = st.matvec_T(b).as_1d_tensor().detach().numpy()
+        gen = torch.Generator().manual_seed(3)
+        v = GaussianModelState.from_gaussians(model, param_mask=param_mask)
+        vv = v.as_1d_tensor()
+        vv.copy_(torch.randn(vv.shape, generator=gen))
+        v.load_1d_tensor(vv)
+        v = GaussianModelState(v.xyz_grad, v.features_dc_grad, v.features_rest_grad, v.scaling_grad, v.rotation_grad,
+                               v.opacity_grad, v.exposure_grad.zero_(), param_mask=param_mask)
+        Av = st.matvec_T(st.matvec(v)) + v * damp
+        out["v"] = v.as_1d_tensor().detach().numpy()
+        out["Av"] = Av.as_1d_tensor().detach().numpy()
+        x0 = st.get_initial_solution()
+        x = cgls_damped(matvec=st.matvec, matvec_T=st.matvec_T, dot=st.dot, saxpy=st.saxpy, b=b, x0=x0, damp=damp,
+                        tol=1e-10, atol=0.0, max_iter=10, restart_iter=10, verbose=False)
+        out["x_ten"] = x.as_1d_tensor().detach().numpy()
+    np.savez(os.path.join(HERE, "solver_ssim_golden.npz"), **out)
+
+
 def solver_golden():
     with reference_on_path():
         from solver.conjugate_gradient import cgls_damped
@@ -210,5 +296,7 @@ if __name__ == "__main__":
     cov_golden()
     camera_golden()
     solver_golden()
+    ssim_golden()
+    solver_ssim_golden()
     raster_fixture()
     print("golden fixtures written to", HERE)

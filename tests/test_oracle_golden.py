@@ -110,3 +110,32 @@ def test_oracle_cgls_matches_reference_schedule(sched, key):
     x = cgls_ref(op, op.rhs(), sched[0], sched[1])
     err = np.linalg.norm(x.numpy().astype(np.float64) - d[key]) / np.linalg.norm(d[key])
     assert err < 1e-3, err
+
+
+def test_ssim_oracle_matches_reference():
+    """oracle/ssim_ref.py's SSIM map equals the reference's utils/loss_utils.py ssim_per_pixel on random
+    pairs and on the solver scene's renders (ssim_golden.npz)."""
+    from oracle import ssim_ref
+    d = _g("ssim_golden.npz")
+    for a, b, ref in (("rand_a", "rand_b", "rand_ssim"), ("scene_x", "scene_gt", "scene_ssim")):
+        got = ssim_ref.ssim_per_pixel(torch.from_numpy(d[a]), torch.from_numpy(d[b])).numpy()
+        assert np.abs(got - d[ref]).max() <= 1e-6, ref
+    assert np.array_equal(np.abs(d["rand_a"] - d["rand_b"]), d["rand_l1"])
+
+
+def test_oracle_ssim_lm_algebra_matches_reference_solver():
+    """The disable_ssim=False residual: loss, J^T b, (J^T J + D) v and 10 CGLS iterations of the
+    oracle equal the reference solver's (solver_ssim_golden.npz)."""
+    from oracle.lm_ref import OracleLMProblem, cgls_ref
+    _, m, cams = _solver_scene()
+    d = _g("solver_ssim_golden.npz")
+    op = OracleLMProblem(m, cams, torch.zeros(3), ssim=True)
+    # the reference's loss_scalar sums r^2 in float32 (loss_image_state.py:16-19), the oracle in float64
+    assert abs(float(op.evaluate()) - float(d["loss"])) <= 1e-5 * float(d["loss"])
+    g = op.rhs()
+    assert _close(g.numpy(), d["Jtb"], 1e-5)
+    y = op.matvec(torch.from_numpy(d["v"]), op.zeros())
+    assert _close(y.numpy(), d["Av"], 1e-5)
+    x = cgls_ref(op, g, 10, 10)
+    err = np.linalg.norm(x.numpy().astype(np.float64) - d["x_ten"]) / np.linalg.norm(d["x_ten"])
+    assert err < 1e-3, err
