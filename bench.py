@@ -210,6 +210,8 @@ def main():
     # ---------------- BASELINE configs[2] as train_jvp.py runs it: one full LM step (loss, J^T b, CGLS with
     # 10 iterations and the reference's residual monitor, 7-point line search on the validation view)
     lm = time_lm_step(model, cams, bg) if world_size == 1 else None
+    # the SSIM residual (disable_ssim=False): CG iteration on the same view(s)
+    ssim = time_ssim_cg(model, cams, bg, steps=args.steps) if world_size == 1 else None
 
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
@@ -254,11 +256,29 @@ def main():
             "cpu_baseline": cpu,
             "raster_fwd_bwd": fb,
             "lm_step": lm,
+            "ssim_cg": ssim,
         }
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_ssim_cg(model, cams, bg, steps=10):
+    """CG iterations of the LM normal equations with the SSIM residual ([r1; r2], lambda_dssim 0.2):
+    per view J v -> image-space factor (separable 11-tap SSIM JVP / VJP) -> seeded VJP -> gather."""
+    from gslm.lm import LMProblem, cgls_fused
+    prob = LMProblem(model, cams, bg, ssim=True)
+    prob.evaluate()
+    g = prob.rhs(prob.zeros())
+    cgls_fused(prob, g, max_iter=2, restart_iter=2, check_every=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    cgls_fused(prob, g, max_iter=steps, restart_iter=steps, check_every=False)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    return {"config": f"CG iteration with the SSIM residual, {len(cams)} view(s) (batch_training_loss.py:18-30)",
+            "ms_per_step": 1e3 * t, "view_matvec_per_s": len(cams) / t}
 
 
 def time_lm_step(model, cams, bg, iters=10, reps=2):

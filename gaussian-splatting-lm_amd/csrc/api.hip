@@ -379,6 +379,21 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   if ((stages & GSLM_STAGE_TANGENT) &&
       (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s)))
     return st;
+  float* jv_out = opts ? opts->jv_out : nullptr;
+  if (jv_out) {
+    if (seed || (stages & (GSLM_STAGE_GATHER | GSLM_STAGE_SCREEN))) {
+      set_error("matvec: jv_out excludes pixel_seed, GATHER and SCREEN");
+      return GSLM_ERR_INVALID;
+    }
+    if (stages & GSLM_STAGE_RENDER) {
+      if (N == 0) {
+        GSLM_HIP_CHECK(hipMemsetAsync(jv_out, 0, (size_t)3 * b.v.H * b.v.W * sizeof(float), s));
+      } else if ((st = launch_render_jv(b.v, t, b.gb, b.bb, b.ib, b.sb, mask_xyz != 0, jv_out, s))) {
+        return st;
+      }
+    }
+    return GSLM_OK;
+  }
   if (seed) {
     if ((stages & GSLM_STAGE_RENDER) &&
         (st = launch_render_vjp_lm(b.v, b.gb, b.bb, b.ib, N, seed, b.sb, opts->flags & GSLM_MV_TAIL_CLEAN, s)))

@@ -376,6 +376,8 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);
+int launch_render_jv(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
+                     const ScratchBufs& sb, bool mask_xyz, float* jv_out, hipStream_t s);
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
                          const ScratchBufs& sb, int64_t N, const float* weight, bool mask_xyz, bool tail_clean,
                          hipStream_t s);

@@ -230,6 +230,19 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
   return GSLM_OK;
 }
 
+int launch_render_jv(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
+                     const ScratchBufs& sb, bool mask_xyz, float* jv_out, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (mask_xyz)
+    hipLaunchKernelGGL(k_render_jvp<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out, (float*)nullptr);
+  else
+    hipLaunchKernelGGL(k_render_jvp<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out, (float*)nullptr);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
                          const ScratchBufs& sb, int64_t N, const float* weight, bool mask_xyz, bool tail_clean,
                          hipStream_t s) {

@@ -57,7 +57,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("dot_scratch", ctypes.c_void_p), ("dot_scratch_bytes", ctypes.c_size_t),
         ("xpby_s", ctypes.c_void_p), ("beta_num", ctypes.c_void_p), ("beta_den", ctypes.c_void_p),
         ("xpby_tail_v", ctypes.c_void_p), ("xpby_tail_s", ctypes.c_void_p), ("xpby_tail_n", ctypes.c_int64),
-        ("screen_out", ctypes.c_void_p), ("pixel_seed", ctypes.c_void_p),
+        ("screen_out", ctypes.c_void_p), ("pixel_seed", ctypes.c_void_p), ("jv_out", ctypes.c_void_p),
     ]
 
 
@@ -123,6 +123,13 @@ EXPORTS = {
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32,
                                         ctypes.c_void_p]),
+    "gslm_ssim_state_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "gslm_ssim_residual": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int32, ctypes.c_void_p]),
+    "gslm_ssim_normal": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_inspect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

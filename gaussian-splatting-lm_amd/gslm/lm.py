@@ -76,8 +76,14 @@ class ViewRaster:
 class LMProblem:
     """The LM normal equations of one camera batch (one LM step's worth of cached geometry)."""
 
-    def __init__(self, model, cams, bg, gts=None, alpha_masks=None, mask_xyz=True, damp=None, device="cuda"):
+    def __init__(self, model, cams, bg, gts=None, alpha_masks=None, mask_xyz=True, damp=None, device="cuda",
+                 ssim=False, lambda_dssim=0.2):
+        """ssim=False: the residual train_jvp.py uses (disable_ssim=True, [r; r]); ssim=True: the
+        [r1; r2] residual with the SSIM term (batch_training_loss.py:18-30, gslm_ssim_*)."""
         self.model = model
+        self.ssim, self.lambda_dssim = bool(ssim), float(lambda_dssim)
+        if self.ssim and not mask_xyz:
+            raise ValueError("the SSIM residual path runs on the LM rows (mask_xyz=True, train_jvp.py:221-227)")
         self.cams = cams
         self.device = device
         self.bg = bg
@@ -97,6 +103,9 @@ class LMProblem:
         self.weights = [None] * len(cams)
         self.residuals = [None] * len(cams)
         self.seeds = [None] * len(cams)
+        self.ssim_state = [None] * len(cams)
+        self._jv = [None] * len(cams)
+        self._u = [None] * len(cams)
         self.res_scratch = torch.empty(lib.gslm_residual_scratch_bytes(1, 1) // 8, dtype=torch.float64,
                                        device=device)
 
@@ -121,6 +130,17 @@ class LMProblem:
             if gt.shape != R.shape or gt.dtype != torch.float32:
                 raise ValueError(f"ground truth must be float32 {tuple(R.shape)}, got {gt.dtype} {tuple(gt.shape)}")
             gt = gt.contiguous()
+            if self.ssim:
+                if self.ssim_state[b] is None:
+                    self.ssim_state[b] = _lib.u8(lib.gslm_ssim_state_bytes(vr.H, vr.W), self.device)
+                    self._jv[b] = torch.empty_like(R)
+                    self._u[b] = torch.empty_like(R)
+                st = self.ssim_state[b]
+                check(lib.gslm_ssim_residual(vr.H, vr.W, R.data_ptr(), gt.data_ptr(),
+                                             None if m is None else m.data_ptr(), self.lambda_dssim, st.data_ptr(),
+                                             st.numel(), None, None, self.seeds[b].data_ptr(), loss.data_ptr(),
+                                             int(b > 0), self.stream), "gslm_ssim_residual")
+                continue
             check(lib.gslm_lm_residual(vr.H, vr.W, R.data_ptr(), gt.data_ptr(), None if m is None else m.data_ptr(),
                                        self.residuals[b].data_ptr(), self.weights[b].data_ptr(),
                                        self.seeds[b].data_ptr(), self.res_scratch.data_ptr(),
@@ -223,6 +243,9 @@ class LMProblem:
                 opts.dot_vy = dot_out
                 opts.dot_scratch = self.dot_scratch.data_ptr()
                 opts.dot_scratch_bytes = self.dot_scratch.numel() * 8
+            if self.ssim:
+                self._ssim_product(b, vr, g, vs, ys, opts)
+                continue
             check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
                                           self.weights[b].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
                                           vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
@@ -234,6 +257,34 @@ class LMProblem:
         else:
             y[e0:e1].zero_()
         return y
+
+    def _ssim_product(self, b, vr, g, vs, ys, opts):
+        """One view's J^T J v with the SSIM residual: J v (jv_out) -> image-space factor
+        M (d1^2 + S^T c2^2 S) M (gslm_ssim_normal) -> seeded back-to-front pass + LM gather.
+        opts carries this view's gather options (overwrite, damping, dot) and the fused xpby."""
+        jv, u = self._jv[b], self._u[b]
+        o1 = _lib.GslmMatvecOpts()
+        o1.stages = 1 | 2  # TANGENT | RENDER
+        o1.jv_out = jv.data_ptr()
+        o1.xpby_s, o1.beta_num, o1.beta_den = opts.xpby_s, opts.beta_num, opts.beta_den
+        o1.xpby_tail_v, o1.xpby_tail_s, o1.xpby_tail_n = opts.xpby_tail_v, opts.xpby_tail_s, opts.xpby_tail_n
+        check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs), jv.data_ptr(), 1,
+                                      vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
+                                      vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o1),
+                                      self.stream), "gslm_matvec_view_ex(jv)")
+        check(lib.gslm_ssim_normal(vr.H, vr.W, self.gts[b].data_ptr(), self.ssim_state[b].data_ptr(), jv.data_ptr(),
+                                   u.data_ptr(), self.stream), "gslm_ssim_normal")
+        o2 = _lib.GslmMatvecOpts()
+        o2.stages = 2 | 4 | (opts.stages & STAGE_OVERWRITE)  # RENDER | GATHER
+        o2.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
+        o2.pixel_seed = u.data_ptr()
+        o2.damp7 = opts.damp7
+        o2.dot_vy, o2.dot_scratch, o2.dot_scratch_bytes = opts.dot_vy, opts.dot_scratch, opts.dot_scratch_bytes
+        check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs), u.data_ptr(), 1,
+                                      vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
+                                      vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o2),
+                                      self.stream), "gslm_matvec_view_ex(seed)")
+        vr.tail_clean = True
 
     # -------------------------------------------------------------- view-sharded exchange (gslm.parallel)
     def views_for(self, cams, pad_to=None):

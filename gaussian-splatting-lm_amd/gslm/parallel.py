@@ -74,7 +74,7 @@ class ShardedOperator:
         if self.world_size == 1 or mode == "allreduce":
             return "allreduce"
         capable = self.all_cams is not None and getattr(self.local, "mask_xyz", False) and \
-            hasattr(self.local, "screen_products")
+            hasattr(self.local, "screen_products") and not getattr(self.local, "ssim", False)
         if mode == "screen":
             if not capable:
                 raise ValueError("screen exchange needs the GPU LMProblem, mask_xyz=True and all_cams")

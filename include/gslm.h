@@ -190,6 +190,10 @@ typedef struct gslm_matvec_opts {
    * (v is then only read for D v / dot_vy).  Needs mask_xyz; excludes TANGENT, SCREEN and xpby.  This
    * is the J^T b of an LM step (train_jvp.py:243, solver_functions.py:101-132) on the fused path. */
   const float* pixel_seed;
+  /* J v only: when set, RENDER runs the front-to-back tangent pass alone and writes the colour tangent
+   * J v ([3,H,W], before the clamp / mask) to jv_out; no rows are written, so GATHER must not be in the
+   * same call.  The SSIM residual's product uses it: J v -> gslm_ssim_normal -> pixel_seed. */
+  float* jv_out;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
@@ -249,6 +253,22 @@ size_t gslm_residual_scratch_bytes(int32_t H, int32_t W);
 int gslm_lm_residual(int32_t H, int32_t W, const float* color, const float* gt, const float* alpha_mask,
                      float* residual, float* weight, float* seed, void* scratch, size_t scratch_bytes,
                      double* loss_dev, int32_t accumulate, void* stream);
+
+/* ---- SSIM residual of the LM step (solver/batch_training_loss.py:18-30 with
+ * disable_ssim=False, FUSED_SSIM_AVAILABLE=False, on utils/loss_utils.py:91-122 ssim_per_pixel) ----
+ * Per view: r1 = a sqrt(|x - gt| + 1e-6), r2 = b sqrt(|1 - SSIM(x, gt)| + 1e-6) with x = m clamp(color, 0, 1),
+ * a = sqrt((1 - lambda) / 3HW), b = sqrt(lambda / 3HW) (batch_training_loss.py:69-77); residual vector
+ * [r1; r2], loss = ||r1||^2 + ||r2||^2.  `state` (gslm_ssim_state_bytes) keeps the linearisation at x.
+ * gslm_ssim_residual: *loss_dev = [*loss_dev if accumulate] + loss; r1 / r2 / seed optional; seed =
+ *   dL/dcolor of J^T b = -M (d1 r1 + S^T c2 r2) (feed it to gslm_matvec_view_ex's pixel_seed).
+ * gslm_ssim_normal: u = M (d1^2 + S^T c2^2 S) M jv, the image-space factor of J^T J: with jv = J v
+ *   (gslm_matvec_opts.jv_out), pixel_seed = u gives J^T J v.  Overwrites the state's scratch plane, so
+ *   call gslm_ssim_residual with seed != NULL before the first gslm_ssim_normal of a geometry. */
+size_t gslm_ssim_state_bytes(int32_t H, int32_t W);
+int gslm_ssim_residual(int32_t H, int32_t W, const float* color, const float* gt, const float* alpha_mask,
+                       float lambda_dssim, void* state, size_t state_bytes, float* r1, float* r2, float* seed,
+                       double* loss_dev, int32_t accumulate, void* stream);
+int gslm_ssim_normal(int32_t H, int32_t W, const float* gt, void* state, const float* jv, float* u, void* stream);
 
 /* ---- diagnostics: device-to-device copies of internal buffers (any output may be NULL) ----
  * point_list [N] u32 (Gaussian id per sorted slot), ranges [ntiles*2] u32, tiles_touched [P] u32,

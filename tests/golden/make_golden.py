@@ -200,6 +200,13 @@ def solver_ssim_golden():
         from solver.solver_functions import LinearSolverFunctions
         from utils.loss_utils import l1_loss_per_pixel, ssim_per_pixel
     model, cams = solver_scene()
+    # Ground truth = independent uniform images (seed 22), not the perturbed render: r1 = a sqrt(|x - gt| + 1e-6)
+    # has d r1 / dx ~ 1 / sqrt(|x - gt|), so pixels where the render is within ~1e-6 of the ground truth
+    # turn 1-ulp render differences into O(1) changes of J^T J; a perturbed-render ground truth has many
+    # such pixels and makes the golden host-dependent (0.3% on (J^T J + D) v between two CPUs).
+    g = torch.Generator().manual_seed(22)
+    for c in cams:
+        c.original_image = torch.rand(3, c.image_height, c.image_width, generator=g)
     loss_func = partial(oracle_batch_loss_ssim, BatchLossImageState=BatchLossImageState,
                         ref=(l1_loss_per_pixel, ssim_per_pixel))
     param_mask = GaussianModelParamGroupMask(mask_xyz=True)
@@ -225,6 +232,8 @@ def solver_ssim_golden():
         x = cgls_damped(matvec=st.matvec, matvec_T=st.matvec_T, dot=st.dot, saxpy=st.saxpy, b=b, x0=x0, damp=damp,
                         tol=1e-10, atol=0.0, max_iter=10, restart_iter=10, verbose=False)
         out["x_ten"] = x.as_1d_tensor().detach().numpy()
+    for i, c in enumerate(cams):
+        out[f"gt{i}"] = c.original_image.numpy()
     np.savez(os.path.join(HERE, "solver_ssim_golden.npz"), **out)
 
 
@@ -292,6 +301,10 @@ def raster_fixture():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:  # e.g. `make_golden.py solver_ssim_golden`
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     sh_golden()
     cov_golden()
     camera_golden()

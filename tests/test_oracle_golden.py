@@ -129,6 +129,8 @@ def test_oracle_ssim_lm_algebra_matches_reference_solver():
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     _, m, cams = _solver_scene()
     d = _g("solver_ssim_golden.npz")
+    for i, c in enumerate(cams):
+        c.original_image = torch.from_numpy(d[f"gt{i}"])
     op = OracleLMProblem(m, cams, torch.zeros(3), ssim=True)
     # the reference's loss_scalar sums r^2 in float32 (loss_image_state.py:16-19), the oracle in float64
     assert abs(float(op.evaluate()) - float(d["loss"])) <= 1e-5 * float(d["loss"])
