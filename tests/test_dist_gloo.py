@@ -43,7 +43,7 @@ def _lm_vector(layout, n):
     return v
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, ssim=False):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -52,7 +52,7 @@ def _worker(rank, world, port, out_path):
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     model, cams = _scene()
     mine = [cams[i] for i in shard_views(len(cams), rank, world)]
-    op = ShardedOperator(OracleLMProblem(model, mine, torch.zeros(3)))
+    op = ShardedOperator(OracleLMProblem(model, mine, torch.zeros(3), ssim=ssim))
     loss = op.evaluate()
     g = op.rhs(op.zeros())
     v = _lm_vector(op.layout, g.numel())
@@ -64,13 +64,15 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_sharded_operator_matches_single_process(tmp_path):
+@pytest.mark.parametrize("ssim", [False, True])
+def test_sharded_operator_matches_single_process(tmp_path, ssim):
+    """Both residuals: disable_ssim=True ([r; r]) and the SSIM residual ([r1; r2])."""
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     out = str(tmp_path / "r0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, _free_port(), out, ssim), nprocs=2, start_method="spawn", join=True)
     got = torch.load(out, weights_only=True)
     model, cams = _scene()
-    op = OracleLMProblem(model, cams, torch.zeros(3))
+    op = OracleLMProblem(model, cams, torch.zeros(3), ssim=ssim)
     loss = op.evaluate()
     g = op.rhs()
     v = _lm_vector(op.layout, g.numel())

@@ -50,7 +50,7 @@ def _run(op, model_layout):
     return {"loss": loss.cpu(), "g": g.cpu(), "y": y.cpu(), "x": x.cpu()}
 
 
-def _worker(rank, world, port, mode, out_path):
+def _worker(rank, world, port, mode, out_path, ssim=False):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,7 +60,7 @@ def _worker(rank, world, port, mode, out_path):
     for c in cams:
         c.to("cuda")
     mine = [cams[i] for i in shard_views(len(cams), rank, world)]
-    op = ShardedLMProblem(model, mine, torch.zeros(3), all_cams=cams, exchange=mode)
+    op = ShardedLMProblem(model, mine, torch.zeros(3), all_cams=cams, exchange=mode, ssim=ssim)
     assert op.exchange == mode
     res = _run(op, op.layout)
     if rank == 0:
@@ -69,17 +69,17 @@ def _worker(rank, world, port, mode, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["screen", "allreduce"])
-def test_sharded_gpu_operator_matches_single_process(tmp_path, mode):
+@pytest.mark.parametrize("mode,ssim", [("screen", False), ("allreduce", False), ("allreduce", True)])
+def test_sharded_gpu_operator_matches_single_process(tmp_path, mode, ssim):
     from gslm.lm import LMProblem
     out = str(tmp_path / "r0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out, ssim), nprocs=2, start_method="spawn", join=True)
     got = torch.load(out, weights_only=True)
     model, cams = _scene()
     model = model.to("cuda")
     for c in cams:
         c.to("cuda")
-    op = LMProblem(model, cams, torch.zeros(3))
+    op = LMProblem(model, cams, torch.zeros(3), ssim=ssim)
     ref = _run(op, op.layout)
     assert abs(float(got["loss"]) - float(ref["loss"])) <= 1e-9 * float(ref["loss"])
     assert torch.allclose(got["g"], ref["g"], rtol=1e-5, atol=1e-7)
