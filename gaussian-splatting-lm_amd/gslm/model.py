@@ -9,7 +9,9 @@ Mirrors the hot-path parts of `scene/gaussian_model.py`:
   * zero_grad         :122-129
   * update_step       :131-139
   * capture / restore :158-190
-Densification, PLY I/O and optimizer setup are out of scope.
+  * create_from_pcd   :236-265  (scales from distCUDA2 = gslm.knn, csrc/knn.hip)
+  * save_ply / load_ply :329-397 (gslm.ply, numpy; plyfile is not a dependency)
+Densification and optimizer setup are out of scope.
 """
 from contextlib import contextmanager
 
@@ -166,6 +168,35 @@ class GaussianModel:
         (self.active_sh_degree, self._xyz, self._features_dc, self._features_rest,
          self._scaling, self._rotation, self._opacity, self.max_radii2D,
          self.xyz_gradient_accum, self.denom, _opt, self.spatial_lr_scale) = model_args
+
+    # ---- initialisation and on-disk formats ----
+    def create_from_pcd(self, points, colors, n_cams=1, spatial_lr_scale=0.0, device="cuda"):
+        """gaussian_model.py:236-265: SH DC from the point colours, scales log(sqrt(mean 3-NN squared
+        distance)) clamped at 1e-7, identity rotations, opacity 0.1, one eye(3, 4) exposure per camera."""
+        from gslm.knn import distCUDA2
+        self.spatial_lr_scale = spatial_lr_scale
+        pts = torch.as_tensor(points, dtype=torch.float32).to(device)
+        rgb = torch.as_tensor(colors, dtype=torch.float32).to(device)
+        P, K = pts.shape[0], (self.max_sh_degree + 1) ** 2
+        features = torch.zeros((P, 3, K), dtype=torch.float32, device=device)
+        features[:, :3, 0] = RGB2SH(rgb)
+        dist2 = torch.clamp_min(distCUDA2(pts), 0.0000001)
+        scales = torch.log(torch.sqrt(dist2))[..., None].repeat(1, 3)
+        rots = torch.zeros((P, 4), device=device)
+        rots[:, 0] = 1
+        opacities = inverse_sigmoid(0.1 * torch.ones((P, 1), dtype=torch.float32, device=device))
+        exposure = torch.eye(3, 4, device=device)[None].repeat(n_cams, 1, 1)
+        self.set_params(pts, features[:, :, 0:1].transpose(1, 2), features[:, :, 1:].transpose(1, 2), scales, rots,
+                        opacities, exposure)
+        return self
+
+    def save_ply(self, path):
+        from gslm.ply import save_ply
+        save_ply(self, path)
+
+    def load_ply(self, path, device="cuda"):
+        from gslm.ply import load_ply
+        return load_ply(self, path, device=device)
 
     def to(self, device):
         rg = self._xyz.requires_grad

@@ -270,6 +270,13 @@ int gslm_ssim_residual(int32_t H, int32_t W, const float* color, const float* gt
                        double* loss_dev, int32_t accumulate, void* stream);
 int gslm_ssim_normal(int32_t H, int32_t W, const float* gt, void* state, const float* jv, float* u, void* stream);
 
+/* ---- distCUDA2 (simple-knn, called at scene/gaussian_model.py:249 to initialise scales) ----
+ * out[i] = mean of the squared distances from point i to its 3 nearest other points (exact; FLT_MAX
+ * for missing neighbours when n < 4).  xyz [n,3] f32.  Synchronises once (bounding box -> grid size).
+ * scratch >= gslm_knn_scratch_bytes(n). */
+size_t gslm_knn_scratch_bytes(int64_t n);
+int gslm_knn3_mean_dist(int64_t n, const float* xyz, float* out, void* scratch, size_t scratch_bytes, void* stream);
+
 /* ---- diagnostics: device-to-device copies of internal buffers (any output may be NULL) ----
  * point_list [N] u32 (Gaussian id per sorted slot), ranges [ntiles*2] u32, tiles_touched [P] u32,
  * final_T [H*W] f32, n_contrib [H*W] u32, render records [P*12] f32. */
