@@ -360,7 +360,8 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
         set_error("matvec: xpby groups of v and s must match");
         return GSLM_ERR_INVALID;
       }
-      xp.p[k] = ww[k] ? pp[k] : nullptr;
+      // with mask_xyz the xyz group is left untouched: it is zero in every LM iterate (s and p alike)
+      xp.p[k] = (ww[k] && !(k == 0 && mask_xyz)) ? pp[k] : nullptr;
       xp.s[k] = ss[k];
       xp.w[k] = ww[k];
     }

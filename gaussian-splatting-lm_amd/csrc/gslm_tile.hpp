@@ -238,6 +238,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
         // <colour, dL/dpix> for every lane, so the record's colour is read with the rest of it (one LDS
         // round trip per entry instead of a second one inside the valid branch)
+        // the record's colour (and inverse depth) read with the rest of it: one LDS round trip per entry
+        // instead of a second one inside the valid branch (the empty asm pins the loads here)
+        asm volatile("" : : "v"(b.z), "v"(b.w), "v"(c.x), "v"(c.y));
         float cd;
         {
 #pragma clang fp contract(fast)

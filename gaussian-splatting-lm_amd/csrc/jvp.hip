@@ -61,6 +61,10 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
     for (int j = __ballot(!done) != 0ull ? it.next() : -1; j >= 0; j = __ballot(!done) != 0ull ? it.next() : -1) {
       const float4 a = s_r0[j], b = s_r1[j], t0 = s_t0[j], t1 = s_t1[j];
       const float2 cc = s_r2[j], t2 = s_t2[j];
+      // all of the entry's primal and tangent record in one LDS round trip (the empty asm pins the
+      // loads here; otherwise the tangent half is fetched inside the branch, a second exposed latency)
+      asm volatile("" : : "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w), "v"(t2.x), "v"(b.z),
+                   "v"(b.w), "v"(cc.x));
       if (!done) {
         const float dx = a.x - pxf, dy = a.y - pyf;
         const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;

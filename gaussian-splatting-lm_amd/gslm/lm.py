@@ -375,6 +375,11 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     n = prob.layout.numel
     dev = prob.device
     st = prob.stream
+    # With the xyz mask (train_jvp.py:221-227) the xyz group is zero in every iterate: the vector
+    # updates and dots run on [lo, n) only (lo rounded down to a float4 boundary for the update kernel).
+    lo = (3 * prob.layout.P // 4) * 4 if getattr(prob, "mask_xyz", False) else 0
+    na = n - lo
+    off = lambda t: t.data_ptr() + 4 * lo
     sc = torch.zeros(16, dtype=torch.float64, device=dev)
     ptr = lambda i: sc.data_ptr() + 8 * i
     GAM, GAMN, DEL, XG, XS = 0, 1, 2, 3, 4  # gamma / gamma' ping-pong between slots 0 and 1
@@ -393,14 +398,14 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             prob.matvec(x, q)
             torch.sub(g, q, out=s)
         p.copy_(s)
-        prob.dot(s, s, ptr(GAM))
+        prob.dot(s[lo:], s[lo:], ptr(GAM))
         stop = False
         pre = None
         for _ in range(restart_iter):
             # [p = s + beta p, deferred from the previous iteration into this product's tangent kernel]
             # q = A p and delta = <p, A p> (= |J p|^2 + p.D.p), fused into the gather when possible
             if not prob.matvec_dot(p, q, ptr(DEL), pre=pre):
-                prob.dot(p, q, ptr(DEL))
+                prob.dot(p[lo:], q[lo:], ptr(DEL))
             if check_every and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
@@ -408,12 +413,12 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 break
             # x += alpha p ; s -= alpha q ; gamma' = <s, s> [; <x, g>, <x, s> for the monitor]  (one pass)
             if check_every:
-                check(lib.gslm_cg_update_monitor(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(),
-                                                 s.data_ptr(), g.data_ptr(), prob.dot_scratch.data_ptr(),
-                                                 prob.dot_scratch.numel() * 8, ptr(GAMN), ptr(XG), ptr(XS), st))
+                check(lib.gslm_cg_update_monitor(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s), off(g),
+                                                 prob.dot_scratch.data_ptr(), prob.dot_scratch.numel() * 8,
+                                                 ptr(GAMN), ptr(XG), ptr(XS), st))
             else:
-                check(lib.gslm_cg_update(n, ptr(GAM), ptr(DEL), p.data_ptr(), q.data_ptr(), x.data_ptr(),
-                                         s.data_ptr(), prob.dot_scratch.data_ptr(), ptr(GAMN), st))
+                check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s),
+                                         prob.dot_scratch.data_ptr(), ptr(GAMN), st))
             # beta = gamma' / gamma; after the slot swap below these are the GAM / GAMN slots
             pre = (s, ptr(GAMN), ptr(GAM))
             if check_every:

@@ -177,7 +177,7 @@ typedef struct gslm_matvec_opts {
    * s + beta v, beta = *beta_num / *beta_den (device doubles), and so does the flat tail
    * xpby_tail_v[0..xpby_tail_n) (the exposure group) from xpby_tail_s.  v's groups must be
    * contiguous per Gaussian (sh_dc_stride 3, sh_rest_stride 3(M-1)) and writable.  Same arithmetic
-   * as gslm_xpby_dev. */
+   * as gslm_xpby_dev.  With mask_xyz the xyz group is not touched (zero in every LM iterate). */
   const gslm_grads* xpby_s;
   const double* beta_num;
   const double* beta_den;
