@@ -371,6 +371,13 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
     xp.tail_s = opts->xpby_tail_s;
     xp.tail_n = opts->xpby_tail_n;
     if (xp.tail_p && !xp.tail_s) { set_error("matvec: xpby tail without s"); return GSLM_ERR_INVALID; }
+    xp.anum = opts->alpha_num;
+    xp.aden = opts->alpha_den;
+    xp.xoff = opts->xpby_x_offset / (int64_t)sizeof(float);
+    if (xp.anum && (!xp.aden || opts->xpby_x_offset % (int64_t)sizeof(float) != 0)) {
+      set_error("matvec: deferred x update needs alpha_den and a float-aligned xpby_x_offset");
+      return GSLM_ERR_INVALID;
+    }
   }
   const float* seed = opts ? opts->pixel_seed : nullptr;
   if (seed && (!mask_xyz || fused_xpby || (stages & (GSLM_STAGE_TANGENT | GSLM_STAGE_SCREEN)))) {

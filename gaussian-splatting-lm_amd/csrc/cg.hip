@@ -110,14 +110,19 @@ __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const doub
   const float4* g4 = reinterpret_cast<const float4*>(g);
   float4* x4 = reinterpret_cast<float4*>(x);
   float4* s4 = reinterpret_cast<float4*>(s);
+  const bool do_x = x != nullptr;  // x == NULL: the x update is deferred into the next xpby
   for (int64_t i = (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n4; i += stride) {
-    const float4 pv = p4[i], qv = q4[i];
-    float4 xv = x4[i], sv = s4[i];
+    const float4 qv = q4[i];
+    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), sv = s4[i];
     float4 gv;
     if (MONITOR) gv = g4[i];
-    xv.x += a * pv.x; xv.y += a * pv.y; xv.z += a * pv.z; xv.w += a * pv.w;
+    if (do_x) {
+      const float4 pv = p4[i];
+      xv = x4[i];
+      xv.x += a * pv.x; xv.y += a * pv.y; xv.z += a * pv.z; xv.w += a * pv.w;
+      x4[i] = xv;
+    }
     sv.x -= a * qv.x; sv.y -= a * qv.y; sv.z -= a * qv.z; sv.w -= a * qv.w;
-    x4[i] = xv;
     s4[i] = sv;
     acc += (double)sv.x * sv.x + (double)sv.y * sv.y + (double)sv.z * sv.z + (double)sv.w * sv.w;
     if (MONITOR) {
@@ -126,8 +131,11 @@ __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const doub
     }
   }
   for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * DOT_THREADS + threadIdx.x; i < n; i += stride) {
-    const float xv = x[i] + a * p[i];
-    x[i] = xv;
+    float xv = 0.f;
+    if (do_x) {
+      xv = x[i] + a * p[i];
+      x[i] = xv;
+    }
     const float sv = s[i] - a * q[i];
     s[i] = sv;
     acc += (double)sv * sv;

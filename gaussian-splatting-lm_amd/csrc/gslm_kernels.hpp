@@ -367,6 +367,11 @@ struct XpbyK {
   float* tail_p;
   const float* tail_s;
   int64_t tail_n;
+  // deferred x update of the previous CG step, applied to the old p first: x += (anum / aden) p, with x at
+  // p + xoff floats for every group and for the tail (anum == NULL: off)
+  const double* anum;
+  const double* aden;
+  int64_t xoff;
 };
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                        const ScratchBufs& sb, const XpbyK* xp, hipStream_t s);

@@ -14,6 +14,8 @@ namespace gslm {
 // per thread), and the flat tail by block 0.  Same arithmetic as k_xpby_dev (bitwise).
 __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_rest) {
   const float b = (float)((*xp.num) / (*xp.den));
+  const bool with_x = xp.anum != nullptr;
+  const float a = with_x ? (float)((*xp.anum) / (*xp.aden)) : 0.f;  // gslm_cg_update's alpha, bitwise
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t nv = min((int64_t)blockDim.x, P - i0);
   constexpr int U = 8;
@@ -30,10 +32,19 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
         sv[u] = e < len ? s[e] : 0.f;
         pv[u] = e < len ? p[e] : 0.f;
       }
+      float xv[U];
+      if (with_x) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
+          xv[u] = e < len ? p[xp.xoff + e] : 0.f;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
         if (e < len) {
+          if (with_x) p[xp.xoff + e] = xv[u] + a * pv[u];
           const float r = sv[u] + b * pv[u];
           p[e] = r;
           if (k == 2) s_rest[e] = r;  // the SH-rest slice stays in LDS for the tangent below
@@ -42,7 +53,11 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
     }
   }
   if (blockIdx.x == 0 && xp.tail_p)
-    for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) xp.tail_p[e] = xp.tail_s[e] + b * xp.tail_p[e];
+    for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) {
+      const float pv = xp.tail_p[e];
+      if (with_x) xp.tail_p[xp.xoff + e] = xp.tail_p[xp.xoff + e] + a * pv;
+      xp.tail_p[e] = xp.tail_s[e] + b * pv;
+    }
 }
 
 template <bool RAW, bool XPBY>

@@ -58,6 +58,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("xpby_s", ctypes.c_void_p), ("beta_num", ctypes.c_void_p), ("beta_den", ctypes.c_void_p),
         ("xpby_tail_v", ctypes.c_void_p), ("xpby_tail_s", ctypes.c_void_p), ("xpby_tail_n", ctypes.c_int64),
         ("screen_out", ctypes.c_void_p), ("pixel_seed", ctypes.c_void_p), ("jv_out", ctypes.c_void_p),
+        ("alpha_num", ctypes.c_void_p), ("alpha_den", ctypes.c_void_p), ("xpby_x_offset", ctypes.c_int64),
     ]
 
 

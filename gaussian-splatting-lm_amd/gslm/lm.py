@@ -216,8 +216,7 @@ class LMProblem:
         vs = self.layout.grads_struct(v)
         ys = self.layout.grads_struct(y)
         if pre is not None and not self.views:
-            s, num, den = pre
-            check(lib.gslm_xpby_dev(v.numel(), s.data_ptr(), num, den, v.data_ptr(), self.stream), "gslm_xpby_dev")
+            self._pre_without_views(v, pre)
             pre = None
         if not self.views:
             y.zero_()
@@ -232,13 +231,7 @@ class LMProblem:
             opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
             opts.damp7 = self._damps if (damp and b == 0) else None
             if pre is not None and b == 0:
-                s, num, den = pre
-                ss = self.layout.grads_struct(s)
-                opts.xpby_s = ctypes.addressof(ss)
-                opts.beta_num, opts.beta_den = num, den
-                opts.xpby_tail_v = v.data_ptr() + 4 * e0
-                opts.xpby_tail_s = s.data_ptr() + 4 * e0
-                opts.xpby_tail_n = e1 - e0
+                ss = self._pre_opts(opts, v, pre)  # noqa: F841  (kept alive for the call)
             if dot_out is not None and b == last:
                 opts.dot_vy = dot_out
                 opts.dot_scratch = self.dot_scratch.data_ptr()
@@ -258,6 +251,31 @@ class LMProblem:
             y[e0:e1].zero_()
         return y
 
+    # pre = (s, beta_num, beta_den[, x, alpha_num, alpha_den]): before the product, [x += alpha v then]
+    # v = s + beta v -- the CG direction update (and the deferred x update) of the previous iteration
+    def _pre_opts(self, opts, v, pre):
+        s, num, den = pre[:3]
+        e0, e1 = self.layout.offsets["exposure"]
+        ss = self.layout.grads_struct(s)
+        opts.xpby_s = ctypes.addressof(ss)
+        opts.beta_num, opts.beta_den = num, den
+        opts.xpby_tail_v = v.data_ptr() + 4 * e0
+        opts.xpby_tail_s = s.data_ptr() + 4 * e0
+        opts.xpby_tail_n = e1 - e0
+        if len(pre) > 3 and pre[3] is not None:
+            x, anum, aden = pre[3:]
+            opts.alpha_num, opts.alpha_den = anum, aden
+            opts.xpby_x_offset = x.data_ptr() - v.data_ptr()
+        return ss
+
+    def _pre_without_views(self, v, pre):
+        s, num, den = pre[:3]
+        if len(pre) > 3 and pre[3] is not None:
+            x, anum, aden = pre[3:]
+            check(lib.gslm_axpy_dev(v.numel(), anum, aden, 1.0, v.data_ptr(), x.data_ptr(), self.stream),
+                  "gslm_axpy_dev")
+        check(lib.gslm_xpby_dev(v.numel(), s.data_ptr(), num, den, v.data_ptr(), self.stream), "gslm_xpby_dev")
+
     def _ssim_product(self, b, vr, g, vs, ys, opts):
         """One view's J^T J v with the SSIM residual: J v (jv_out) -> image-space factor
         M (d1^2 + S^T c2^2 S) M (gslm_ssim_normal) -> seeded back-to-front pass + LM gather.
@@ -268,6 +286,7 @@ class LMProblem:
         o1.jv_out = jv.data_ptr()
         o1.xpby_s, o1.beta_num, o1.beta_den = opts.xpby_s, opts.beta_num, opts.beta_den
         o1.xpby_tail_v, o1.xpby_tail_s, o1.xpby_tail_n = opts.xpby_tail_v, opts.xpby_tail_s, opts.xpby_tail_n
+        o1.alpha_num, o1.alpha_den, o1.xpby_x_offset = opts.alpha_num, opts.alpha_den, opts.xpby_x_offset
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs), jv.data_ptr(), 1,
                                       vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                       vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o1),
@@ -305,21 +324,14 @@ class LMProblem:
         ys = self.layout.grads_struct(v)  # unused by the SCREEN stage
         e0, e1 = self.layout.offsets["exposure"]
         if pre is not None and not self.views:
-            s, num, den = pre
-            check(lib.gslm_xpby_dev(v.numel(), s.data_ptr(), num, den, v.data_ptr(), self.stream), "gslm_xpby_dev")
+            self._pre_without_views(v, pre)
         for b, vr in enumerate(self.views):
             opts = _lib.GslmMatvecOpts()
             opts.stages = 1 | 2 | 16  # TANGENT | RENDER | SCREEN
             opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
             opts.screen_out = screen[b].data_ptr()
             if pre is not None and b == 0:
-                s, num, den = pre
-                ss = self.layout.grads_struct(s)
-                opts.xpby_s = ctypes.addressof(ss)
-                opts.beta_num, opts.beta_den = num, den
-                opts.xpby_tail_v = v.data_ptr() + 4 * e0
-                opts.xpby_tail_s = s.data_ptr() + 4 * e0
-                opts.xpby_tail_n = e1 - e0
+                ss = self._pre_opts(opts, v, pre)  # noqa: F841
             check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
                                           self.weights[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
@@ -389,12 +401,24 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     q = torch.zeros_like(x)
     b2 = float(prob.loss) if check_every else None  # ||b||^2 = loss
     iter_total, last_res, history = 0, math.inf, []
+    # Benchmark mode defers x += alpha p into the next product's xpby pass (gslm_matvec_opts.alpha_num):
+    # the update kernel then streams s and q only; the iterates are bitwise those of the undeferred loop.
+    defer = not check_every and callback is None
+    pend = None  # (alpha_num, alpha_den) of a deferred x update not yet applied
+
+    def flush():
+        nonlocal pend
+        if pend is not None:
+            check(lib.gslm_axpy_dev(na, pend[0], pend[1], 1.0, off(p), off(x), st), "gslm_axpy_dev")
+            pend = None
+
     first = True
     while iter_total < max_iter:
         if first:
             s.copy_(g)  # s0 = J^T b - D x0 with x0 = 0
             first = False
         else:
+            flush()
             prob.matvec(x, q)
             torch.sub(g, q, out=s)
         p.copy_(s)
@@ -402,20 +426,27 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
         stop = False
         pre = None
         for _ in range(restart_iter):
-            # [p = s + beta p, deferred from the previous iteration into this product's tangent kernel]
+            # [p = s + beta p and the deferred x += alpha p, both fused into this product's tangent kernel]
             # q = A p and delta = <p, A p> (= |J p|^2 + p.D.p), fused into the gather when possible
-            if not prob.matvec_dot(p, q, ptr(DEL), pre=pre):
+            full = None if pre is None else pre + ((x, pend[0], pend[1]) if pend is not None else (None, None, None))
+            if full is not None:
+                pend = None
+            if not prob.matvec_dot(p, q, ptr(DEL), pre=full):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
             if check_every and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
                 stop = True
                 break
-            # x += alpha p ; s -= alpha q ; gamma' = <s, s> [; <x, g>, <x, s> for the monitor]  (one pass)
+            # [x += alpha p ;] s -= alpha q ; gamma' = <s, s> [; <x, g>, <x, s> for the monitor]  (one pass)
             if check_every:
                 check(lib.gslm_cg_update_monitor(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s), off(g),
                                                  prob.dot_scratch.data_ptr(), prob.dot_scratch.numel() * 8,
                                                  ptr(GAMN), ptr(XG), ptr(XS), st))
+            elif defer:
+                check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), None, off(s),
+                                         prob.dot_scratch.data_ptr(), ptr(GAMN), st))
+                pend = (ptr(GAM), ptr(DEL))  # alpha = gamma / delta, read before either slot is rewritten
             else:
                 check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s),
                                          prob.dot_scratch.data_ptr(), ptr(GAMN), st))
@@ -443,6 +474,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 break
         if stop:
             break
+    flush()
     return x, {"iters": iter_total, "residuals": history}
 
 

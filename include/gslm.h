@@ -194,6 +194,13 @@ typedef struct gslm_matvec_opts {
    * J v ([3,H,W], before the clamp / mask) to jv_out; no rows are written, so GATHER must not be in the
    * same call.  The SSIM residual's product uses it: J v -> gslm_ssim_normal -> pixel_seed. */
   float* jv_out;
+  /* Deferred x update of the previous CG step (conjugate_gradient.py:95 x += alpha p), fused with xpby:
+   * when alpha_num is set, every element of v (groups and tail) first adds (alpha_num / alpha_den) v into
+   * x, where x lives xpby_x_offset bytes from v (x and v two flat vectors of the same layout).  Same
+   * arithmetic as gslm_cg_update's x update, so the iterates are bitwise those of the undeferred loop. */
+  const double* alpha_num;
+  const double* alpha_den;
+  int64_t xpby_x_offset;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
@@ -226,7 +233,9 @@ int gslm_axpy_dev(int64_t n, const double* num_dev, const double* den_dev, float
 int gslm_xpby_dev(int64_t n, const float* s, const double* num_dev, const double* den_dev, float* p,
                   void* stream);
 /* One CG step, a = gam / del read from device memory:  x += a p;  s -= a q;
- * *gam_new_dev = <s, s> (scratch >= gslm_dot_scratch_bytes(n)).  Vectors 16-byte aligned. */
+ * *gam_new_dev = <s, s> (scratch >= gslm_dot_scratch_bytes(n)).  Vectors 16-byte aligned.
+ * x == NULL: only s -= a q and <s, s> (the x update deferred into the next product's xpby, see
+ * gslm_matvec_opts.alpha_num; p is then not read). */
 int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                    float* x, float* s, void* scratch, double* gam_new_dev, void* stream);
 /* gslm_cg_update plus the residual monitor of conjugate_gradient.py:103-104 in the same pass:
