@@ -214,6 +214,71 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(SsimWin w, int H, int W, const
   sep_conv_tile<3>(w, H, W, lds, src, epi);
 }
 
+// ---- the first-order training loss's SSIM term (train.py:121-125, utils/loss_utils.py:59-89 `ssim`, the
+// role upstream's optional fused_ssim plays): mean SSIM of C channel planes and its gradient.
+//   dmean(S)/dx = (1/n) [K*(a1) + 2 x K*(a2) + y K*(a3)]   (the S^T w of the LM path with w = 1).
+// The forward stores a1, a2, a3 ([3][C H W] floats) for the backward.
+__global__ __launch_bounds__(256) void k_ssim_mean(SsimWin w, int H, int W, int C, const float* __restrict__ x,
+                                                   const float* __restrict__ y, float* __restrict__ planes,
+                                                   double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double s_red[4];
+  const int64_t NC = (int64_t)C * H * W;
+  const int64_t HW = (int64_t)H * W;
+  double acc = 0.0;
+  auto src = [&](int c, int yy, int xx, float v[5]) {
+    const int64_t k = c * HW + (int64_t)yy * W + xx;
+    const float a = x[k], b = y[k];
+    v[0] = a; v[1] = b; v[2] = a * a; v[3] = b * b; v[4] = a * b;
+  };
+  auto epi = [&](int c, int yy, int xx, int64_t k, const float v[5]) {
+    // utils/loss_utils.py:70-84 operation order
+    const float mu1 = v[0], mu2 = v[1];
+    const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
+    const float s1 = v[2] - mu1_sq, s2 = v[3] - mu2_sq, s12 = v[4] - mu1_mu2;
+    const float A = 2.f * mu1_mu2 + SS_C1, B = 2.f * s12 + SS_C2;
+    const float Cc = (mu1_sq + mu2_sq) + SS_C1, D = (s1 + s2) + SS_C2;
+    const float S = (A * B) / (Cc * D);
+    const float CD = Cc * D;
+    planes[0 * NC + k] = 2.f * mu2 * (B - A) / CD - 2.f * S * mu1 * (1.f / Cc - 1.f / D);
+    planes[1 * NC + k] = -S / D;
+    planes[2 * NC + k] = 2.f * A / CD;
+    acc += (double)S;
+  };
+  sep_conv_tile<5>(w, H, W, lds, src, epi);
+  const double t = block_sum_256(acc, s_red);
+  if (threadIdx.x == 0)
+    part[((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_ssim_mean_final(const double* __restrict__ part, int np, double inv_n,
+                                                         float* __restrict__ out) {
+  __shared__ double s[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  const double t = block_sum_256(acc, s);
+  if (threadIdx.x == 0) *out = (float)(t * inv_n);
+}
+
+// grad = (*gscale / n) [K*(a1) + 2 x K*(a2) + y K*(a3)]
+__global__ __launch_bounds__(256) void k_ssim_mean_bwd(SsimWin w, int H, int W, int C, const float* __restrict__ x,
+                                                       const float* __restrict__ y, const float* __restrict__ planes,
+                                                       const float* __restrict__ gscale, float inv_n,
+                                                       float* __restrict__ grad) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int64_t NC = (int64_t)C * H * W;
+  const int64_t HW = (int64_t)H * W;
+  const float sc = *gscale * inv_n;
+  auto src = [&](int c, int yy, int xx, float v[3]) {
+    const int64_t k = c * HW + (int64_t)yy * W + xx;
+    v[0] = planes[k]; v[1] = planes[NC + k]; v[2] = planes[2 * NC + k];
+  };
+  auto epi = [&](int c, int yy, int xx, int64_t k, const float v[3]) {
+    grad[k] = sc * ((v[0] + (2.f * x[k]) * v[1]) + y[k] * v[2]);
+  };
+  sep_conv_tile<3>(w, H, W, lds, src, epi);
+}
+
 static SsimWin make_window() {
   // utils/loss_utils.py:49-51: exp in double, a float32 tensor, normalised by its float32 sum
   SsimWin w;
@@ -226,8 +291,8 @@ static SsimWin make_window() {
   return w;
 }
 
-static dim3 ssim_grid(int H, int W) {
-  return dim3((unsigned)((W + SS_TW - 1) / SS_TW), (unsigned)((H + SS_TH - 1) / SS_TH), 3u);
+static dim3 ssim_grid(int H, int W, int C = 3) {
+  return dim3((unsigned)((W + SS_TW - 1) / SS_TW), (unsigned)((H + SS_TH - 1) / SS_TH), (unsigned)C);
 }
 
 }  // namespace gslm
@@ -286,6 +351,44 @@ int gslm_ssim_normal(int32_t H, int32_t W, const float* gt, void* state, const f
   hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(256), sep_conv_lds<3>(), s, w, H, W, gt, (float*)state, jv);
   GSLM_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(256), sep_conv_lds<3>(), s, w, H, W, gt, (const float*)state, jv, 1.0f, u);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+size_t gslm_ssim_mean_state_bytes(int32_t C, int32_t H, int32_t W) {
+  const size_t n = (size_t)(C > 0 ? C : 0) * (size_t)(H > 0 ? H : 0) * (size_t)(W > 0 ? W : 0);
+  const dim3 g = ssim_grid(H > 0 ? H : 1, W > 0 ? W : 1, C > 0 ? C : 1);
+  return align_up(3 * n * sizeof(float), 16) + ((size_t)g.x * g.y * g.z + 16) * sizeof(double);
+}
+
+int gslm_ssim_mean(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, void* state,
+                   size_t state_bytes, float* ssim_out, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0) { set_error("ssim_mean: empty image"); return GSLM_ERR_INVALID; }
+  if (!img || !gt || !state || !ssim_out) { set_error("ssim_mean: NULL argument"); return GSLM_ERR_INVALID; }
+  if (state_bytes < gslm_ssim_mean_state_bytes(C, H, W)) { set_error("ssim_mean: state too small"); return GSLM_ERR_CAPACITY; }
+  hipStream_t s = (hipStream_t)stream;
+  const SsimWin w = make_window();
+  const dim3 grid = ssim_grid(H, W, C);
+  const size_t n = (size_t)C * H * W;
+  double* part = (double*)((char*)state + align_up(3 * n * sizeof(float), 16));
+  hipLaunchKernelGGL(k_ssim_mean, grid, dim3(256), sep_conv_lds<5>(), s, w, H, W, C, img, gt, (float*)state, part);
+  GSLM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_ssim_mean_final, dim3(1), dim3(256), 0, s, part, (int)(grid.x * grid.y * grid.z),
+                     1.0 / (double)n, ssim_out);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_ssim_mean_backward(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, const void* state,
+                            const float* grad_out, float* grad_img, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0) { set_error("ssim_mean_backward: empty image"); return GSLM_ERR_INVALID; }
+  if (!img || !gt || !state || !grad_out || !grad_img) { set_error("ssim_mean_backward: NULL argument"); return GSLM_ERR_INVALID; }
+  hipStream_t s = (hipStream_t)stream;
+  const SsimWin w = make_window();
+  const dim3 grid = ssim_grid(H, W, C);
+  const float inv_n = (float)(1.0 / ((double)C * H * W));
+  hipLaunchKernelGGL(k_ssim_mean_bwd, grid, dim3(256), sep_conv_lds<3>(), s, w, H, W, C, img, gt,
+                     (const float*)state, grad_out, inv_n, grad_img);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

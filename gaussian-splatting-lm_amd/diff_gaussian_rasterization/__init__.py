@@ -12,8 +12,13 @@ Same surface as the package the reference imports at gaussian_renderer/__init__.
 
 The autograd Function implements `backward` (VJP, -> libgslm gslm_backward) and forward-mode `jvp`
 (-> gslm_jvp, reusing the forward's sorted tile lists), which the reference's LM solver drives
-through torch.autograd.forward_ad (solver/solver_functions.py:86-92).  SparseGaussianAdam is NOT
-exported, so `train_jvp.py` keeps separate_sh=False (train_jvp.py:50-54).
+through torch.autograd.forward_ad (solver/solver_functions.py:86-92).
+
+`SparseGaussianAdam` (gslm.optim, one HIP launch per step) is exported as the accelerated upstream
+rasterizer exports it (train.py:37-41, gaussian_model.py:29).  Its presence makes the reference's
+train.py / train_jvp.py call render(..., separate_sh=True), which passes `dc=` and the SH rest
+separately (gaussian_renderer/__init__.py:82-100): the rasterizer reads both in place (forward, VJP and
+forward-mode JVP), so the LM path is unchanged by it.
 """
 import ctypes
 from typing import NamedTuple
@@ -24,7 +29,9 @@ import torch.nn as nn
 from gslm import _lib
 from gslm._lib import lib, check
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+from gslm.optim import SparseGaussianAdam  # noqa: E402,F401
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -216,7 +223,8 @@ class GaussianRasterizer(nn.Module):
         shs, colors_precomp = _none_if_empty(shs), _none_if_empty(colors_precomp)
         scales, rotations, cov3D_precomp = _none_if_empty(scales), _none_if_empty(rotations), _none_if_empty(cov3D_precomp)
         dc = _none_if_empty(dc)
-        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+        has_sh = shs is not None or dc is not None  # separate_sh at SH degree 0: dc= with an empty rest
+        if (not has_sh and colors_precomp is None) or (has_sh and colors_precomp is not None):
             raise Exception("Please provide excatly one of either SHs or precomputed colors!")
         if ((scales is None or rotations is None) and cov3D_precomp is None) or (
                 (scales is not None or rotations is not None) and cov3D_precomp is not None):

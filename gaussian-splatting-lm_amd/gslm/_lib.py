@@ -62,6 +62,17 @@ class GslmMatvecOpts(ctypes.Structure):
     ]
 
 
+class GslmAdamGroup(ctypes.Structure):
+    _fields_ = [
+        ("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64), ("floats_per_gaussian", ctypes.c_int32),
+        ("_pad", ctypes.c_int32), ("lr", ctypes.c_double), ("step", ctypes.c_int64),
+    ]
+
+
+ADAM_MAX_GROUPS = 8  # GSLM_ADAM_MAX_GROUPS
+
+
 # Every symbol include/gslm.h declares; tests check the library exports each of them.
 EXPORTS = {
     "gslm_geom_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
@@ -131,9 +142,20 @@ EXPORTS = {
                                           ctypes.c_int32, ctypes.c_void_p]),
     "gslm_ssim_normal": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_ssim_mean_state_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "gslm_ssim_mean": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_ssim_mean_backward": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
     "gslm_knn_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gslm_knn3_mean_dist": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_size_t, ctypes.c_void_p]),
+    "gslm_adam_step": (ctypes.c_int, [ctypes.POINTER(GslmAdamGroup), ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_void_p]),
+    "gslm_densify_stats": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_inspect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

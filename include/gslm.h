@@ -279,12 +279,53 @@ int gslm_ssim_residual(int32_t H, int32_t W, const float* color, const float* gt
                        double* loss_dev, int32_t accumulate, void* stream);
 int gslm_ssim_normal(int32_t H, int32_t W, const float* gt, void* state, const float* jv, float* u, void* stream);
 
+/* ---- the first-order loss's SSIM term (train.py:121-125 ssim(image, gt) = utils/loss_utils.py:59-89 with
+ * size_average; upstream's optional fused_ssim plays this role) ----
+ * img, gt [C,H,W] f32.  gslm_ssim_mean: *ssim_out (device f32) = mean of the SSIM map (11-tap Gaussian
+ * window, sigma 1.5, zero padding), and `state` keeps the map's linearisation for the backward.
+ * gslm_ssim_mean_backward: grad_img = *grad_out * d mean(SSIM) / d img (grad_out: device f32 scalar). */
+size_t gslm_ssim_mean_state_bytes(int32_t C, int32_t H, int32_t W);
+int gslm_ssim_mean(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, void* state,
+                   size_t state_bytes, float* ssim_out, void* stream);
+int gslm_ssim_mean_backward(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, const void* state,
+                            const float* grad_out, float* grad_img, void* stream);
+
 /* ---- distCUDA2 (simple-knn, called at scene/gaussian_model.py:249 to initialise scales) ----
  * out[i] = mean of the squared distances from point i to its 3 nearest other points (exact; FLT_MAX
  * for missing neighbours when n < 4).  xyz [n,3] f32.  Synchronises once (bounding box -> grid size).
  * scratch >= gslm_knn_scratch_bytes(n). */
 size_t gslm_knn_scratch_bytes(int64_t n);
 int gslm_knn3_mean_dist(int64_t n, const float* xyz, float* out, void* scratch, size_t scratch_bytes, void* stream);
+
+/* ---- first-order training step ----
+ * One parameter group of GaussianModel.training_setup (scene/gaussian_model.py:273-280: xyz, f_dc, f_rest,
+ * opacity, scaling, rotation; the exposure optimizer of :291 is one more group).  grad == NULL skips the
+ * group (torch.optim skips parameters whose .grad is None). */
+#define GSLM_ADAM_MAX_GROUPS 8
+typedef struct gslm_adam_group {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;                   /* floats in the group */
+  int32_t floats_per_gaussian; /* sparse: n == floats_per_gaussian * num_gaussians */
+  int32_t _pad;
+  double lr;                   /* param_group["lr"] */
+  int64_t step;                /* dense: state["step"] after its increment (bias correction 1 - beta^step) */
+} gslm_adam_group;
+/* sparse == 0: torch.optim.Adam(params, lr, eps) step (train.py:184-186) -- its foreach arithmetic in f32:
+ *   m += (1-b1)(g-m); v = v b2 + (1-b2) g g; p += (-lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps).
+ * sparse != 0: SparseGaussianAdam.step(visible, num_gaussians) (train.py:180-183; gaussian_model.py:29,286,
+ *   upstream 3dgs_accel rasterizer, absent): elements of Gaussians with visible[g] == 0 untouched, others
+ *   m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p += -lr m / (sqrt(v) + eps)  (no bias correction).
+ * One launch for all groups. */
+int gslm_adam_step(const gslm_adam_group* groups, int32_t ngroups, double beta1, double beta2, double eps,
+                   const uint8_t* visible, int64_t num_gaussians, int32_t sparse, void* stream);
+/* train.py:166-167 (gaussian_model.py:561-563) fused, for the Gaussians with radii > 0 (render()'s
+ * visibility_filter): max_radii2D = max(max_radii2D, radii) (skipped when max_radii2D is NULL),
+ * xyz_gradient_accum += ||means2D_grad[i, 0:2]||, denom += 1.  means2D_grad rows are grad_stride floats. */
+int gslm_densify_stats(int64_t P, const float* means2D_grad, int64_t grad_stride, const int32_t* radii,
+                       float* max_radii2D, float* xyz_gradient_accum, float* denom, void* stream);
 
 /* ---- diagnostics: device-to-device copies of internal buffers (any output may be NULL) ----
  * point_list [N] u32 (Gaussian id per sorted slot), ranges [ntiles*2] u32, tiles_touched [P] u32,

@@ -21,6 +21,11 @@ What is pinned by the *reference's code* (imported from /root/reference, never c
   * solver_ssim_golden.npz  the same solver run with the disable_ssim=False residual
                        (solver/batch_training_loss.py:18-30, restated around the reference's own
                        l1_loss_per_pixel / ssim_per_pixel): loss, J^T b, (J^T J + D) v, 10-iteration CGLS
+  * train_golden.npz   the first-order step: utils/general_utils.py get_expon_lr_func
+                       at the schedules GaussianModel.training_setup builds (scene/gaussian_model.py:293-301,
+                       OptimizationParams defaults of arguments/__init__.py:76-90), and the trajectory of
+                       torch.optim.Adam -- the optimizer the reference steps (gaussian_model.py:283,
+                       train.py:184-186) -- over the six parameter groups with their default lrs
 The rasterizer itself has no reference binary here (absent submodule): its numerics are pinned by
 the oracle restatement, finite differences and the adjoint identity (tests/test_oracle.py).
 """
@@ -285,6 +290,48 @@ def solver_golden():
     np.savez(os.path.join(HERE, "solver_golden.npz"), **out)
 
 
+TRAIN_STEPS = [0, 1, 2, 10, 100, 500, 1000, 7000, 15000, 29999, 30000, 45000]
+ADAM_P = 37  # odd: every group's float count is exercised with a ragged float4 tail
+
+
+def train_golden():
+    with reference_on_path():
+        from utils.general_utils import get_expon_lr_func
+    out = {"steps": np.array(TRAIN_STEPS)}
+    # position schedule (spatial_lr_scale 2.5), exposure schedule (delay 0), and a delayed variant
+    scheds = {"xyz": get_expon_lr_func(0.00016 * 2.5, 0.0000016 * 2.5, lr_delay_mult=0.01, max_steps=30_000),
+              "exposure": get_expon_lr_func(0.01, 0.001, lr_delay_steps=0, lr_delay_mult=0.0, max_steps=30_000),
+              "delayed": get_expon_lr_func(0.01, 0.001, lr_delay_steps=1000, lr_delay_mult=0.1, max_steps=30_000)}
+    for k, f in scheds.items():
+        out[f"lr_{k}"] = np.array([f(s) for s in TRAIN_STEPS], np.float64)
+    # torch.optim.Adam over the training_setup groups (lr as gaussian_model.py:273-280 with the defaults)
+    g = torch.Generator().manual_seed(31)
+    P = ADAM_P
+    shapes = {"xyz": (P, 3), "f_dc": (P, 1, 3), "f_rest": (P, 15, 3), "opacity": (P, 1), "scaling": (P, 3),
+              "rotation": (P, 4)}
+    lrs = {"xyz": 0.00016 * 2.5, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 0.025, "scaling": 0.005,
+           "rotation": 0.001}
+    params = {k: torch.nn.Parameter(torch.randn(shp, generator=g)) for k, shp in shapes.items()}
+    for k, t in params.items():
+        out[f"adam_p0_{k}"] = t.detach().numpy().copy()
+    opt = torch.optim.Adam([{"params": [params[k]], "lr": lrs[k], "name": k} for k in shapes], lr=0.0, eps=1e-15)
+    n_steps = 4
+    for it in range(n_steps):
+        for k, t in params.items():
+            gr = torch.randn(t.shape, generator=g) * (10.0 ** (it - 2))
+            out[f"adam_g{it}_{k}"] = gr.numpy()
+            t.grad = gr
+        opt.step()
+    for k, t in params.items():
+        st = opt.state[t]
+        out[f"adam_p_{k}"] = t.detach().numpy().copy()
+        out[f"adam_m_{k}"] = st["exp_avg"].numpy().copy()
+        out[f"adam_v_{k}"] = st["exp_avg_sq"].numpy().copy()
+        out[f"adam_lr_{k}"] = np.array(lrs[k])
+    out["adam_steps"] = np.array(n_steps)
+    np.savez(os.path.join(HERE, "train_golden.npz"), **out)
+
+
 def raster_fixture():
     """Oracle forward outputs of BASELINE config 1 (2k Gaussians, SH0, 256x256): a regression fixture
     of the restatement itself (not a reference-binary vector, see module docstring)."""
@@ -311,5 +358,6 @@ if __name__ == "__main__":
     solver_golden()
     ssim_golden()
     solver_ssim_golden()
+    train_golden()
     raster_fixture()
     print("golden fixtures written to", HERE)

@@ -63,7 +63,9 @@ def test_dropin_modules_import_with_reference_names():
     assert b.BatchGaussianRasterizationSettings._fields[:5] == (
         "batch_size", "image_heights", "image_widths", "tanfovxs", "tanfovys")
     assert o.GaussianRasterizer is d.GaussianRasterizer
-    assert not hasattr(d, "SparseGaussianAdam")  # keeps train_jvp.py on separate_sh=False
+    # exported like the accelerated upstream rasterizer's (train.py:37-41): render() then passes dc= separately
+    from gslm.optim import SparseGaussianAdam
+    assert d.SparseGaussianAdam is SparseGaussianAdam and issubclass(SparseGaussianAdam, __import__("torch").optim.Adam)
 
 
 def test_rasterizer_argument_validation():
