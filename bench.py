@@ -220,6 +220,10 @@ def main():
     # the SSIM residual (disable_ssim=False): CG iteration on the same view(s)
     ssim = time_ssim_cg(model, cams[:1], bg, steps=args.steps) if world_size == 1 else None
 
+    # first-order path: the fused Adam step at the bench model's size and one train.py
+    # iteration (render, L1 + SSIM loss, backward, densification statistics, Adam) at configs[1]'s size
+    fo = time_first_order(device, W, H, args.s0, P_adam=args.P, sh=args.sh) if rank == 0 else None
+
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -264,11 +268,66 @@ def main():
             "raster_fwd_bwd": fb,
             "lm_step": lm,
             "ssim_cg": ssim,
+            "first_order": fo,
         }
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _events_ms(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def time_first_order(device, W, H, s0, P_adam=1_000_000, sh=3, P_train=100_000, reps=10):
+    """gslm_adam_step (FusedAdam) vs torch.optim.Adam (foreach) over the six training_setup groups of a
+    P_adam-Gaussian model, and one train.py iteration (gslm.train.Trainer.step, no densification) at
+    P_train Gaussians, one WxH view."""
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    from gslm.optim import FusedAdam
+    from gslm.train import OptimizationParams, Trainer
+    K = (sh + 1) ** 2
+    shapes = {"xyz": (P_adam, 3), "f_dc": (P_adam, 1, 3), "f_rest": (P_adam, K - 1, 3), "opacity": (P_adam, 1),
+              "scaling": (P_adam, 3), "rotation": (P_adam, 4)}
+    out = {}
+    for name, cls in (("fused", FusedAdam), ("torch", torch.optim.Adam)):
+        ps = [torch.nn.Parameter(torch.randn(s_, device=device)) for s_ in shapes.values()]
+        for p in ps:
+            p.grad = torch.randn_like(p)
+        opt = cls([{"params": [p], "lr": 1e-3} for p in ps], lr=0.0, eps=1e-15)
+        out[name] = _events_ms(opt.step, reps)
+        del ps, opt
+    floats = sum(math.prod(s_) for s_ in shapes.values())
+    adam = {"config": f"Adam step over the 6 parameter groups of {P_adam} Gaussians SH{sh} ({floats} floats)",
+            "fused_ms": out["fused"], "torch_foreach_ms": out["torch"],
+            "fused_gbs": 28.0 * floats / (out["fused"] * 1e-3) / 1e9,
+            "note": "28 B per float (read p, g, m, v; write p, m, v) over the fused launch's time"}
+    torch.cuda.empty_cache()
+    m = synthetic_gaussians(P_train, sh, seed=0, s0=s0, device="cpu").to(device)
+    m.spatial_lr_scale = 1.0
+    cam = orbit_cameras(1, W, H, seed=1)[0].to(device)
+    cam.original_image = torch.rand(3, H, W, device=device)
+    opt = OptimizationParams(densify_from_iter=10 ** 9)  # statistics every step, no densification
+    m.training_setup(opt)
+    tr = Trainer(m, [cam], opt=opt)
+    it = [1]
+
+    def step():
+        tr.step(it[0], viewpoint_cam=cam)
+        it[0] += 1
+    t_ms = _events_ms(step, reps)
+    return {"adam": adam, "train_step": {
+        "config": f"one train.py iteration, {P_train} Gaussians SH{sh}, 1x{W}x{H} view: render + "
+                  "(1-l) L1 + l (1-SSIM) + backward + densification statistics + Adam", "ms": t_ms}}
 
 
 def time_ssim_cg(model, cams, bg, steps=10):
