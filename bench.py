@@ -96,7 +96,9 @@ def main():
     del gt_prob, pert
 
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
-    prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device)
+    # one view per problem (N = 1): the SH-rest group of the CG vectors is carried as its 3 coordinates in
+    # the view's SH-rest span (GSLM_MV_SH_REST_PROJECTED); several views: the full layout
+    prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device, sh_projection="auto")
     prob.evaluate()
     g = prob.rhs(prob.zeros())
     torch.cuda.synchronize()
@@ -123,6 +125,24 @@ def main():
     barrier()
     t_cg = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = 1e3 * t_cg / args.steps
+
+    # the same CG loop on the reference's full param-space layout (59 floats per Gaussian at SH 3), for
+    # comparison when the projected SH-rest layout ran above
+    cg_full = None
+    if prob.layout.rest_projected:
+        pf = LMProblem(model, cams, bg, device=device, sh_projection=False)
+        pf.evaluate()
+        gf = pf.rhs(pf.zeros())
+        cgls_fused(pf, gf, max_iter=max(args.warmup, 1), restart_iter=max(args.warmup, 1), check_every=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cgls_fused(pf, gf, max_iter=args.steps, restart_iter=args.steps, check_every=False)
+        torch.cuda.synchronize()
+        tf = time.perf_counter() - t0
+        cg_full = {"ms_per_step": 1e3 * tf / args.steps, "view_matvec_per_s": n_views * args.steps / tf,
+                   "note": "CG iteration with the SH-rest group in the reference's layout (3(K-1) floats per Gaussian)"}
+        del pf, gf
+        torch.cuda.empty_cache()
 
     # ---------------- raster Mpix/s: full forwards (preprocess, sort, binning, blend; includes the
     # num_rendered read-back the upstream forward also does)
@@ -151,7 +171,7 @@ def main():
     def stage(mask):
         opts = _lib.GslmMatvecOpts()
         opts.stages = mask | (8 if mask == 4 else 0)  # the gather in its CG form: overwrite + D v
-        opts.flags = 1 if mask == 2 else 0  # GSLM_MV_TAIL_CLEAN: as inside the CG loop (first call below)
+        opts.flags = (1 if mask == 2 else 0) | prob.mv_flags  # GSLM_MV_TAIL_CLEAN: as inside the CG loop
         opts.damp7 = prob._damps if mask == 4 else None
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
                                       prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
@@ -161,6 +181,7 @@ def main():
     stage(1)
     opts0 = _lib.GslmMatvecOpts()
     opts0.stages = 2  # RENDER once with the tail rows written: the state every CG iteration after the first sees
+    opts0.flags = prob.mv_flags
     check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs), prob.weights[0].data_ptr(),
                                   1, vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                   vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts0),
@@ -206,6 +227,7 @@ def main():
     # the side measurements below run on one view and need the memory of the batch's problem back
     # (at configs[4], 5M Gaussians x 32 4K views, that is ~100 GB)
     n_views_local = len(prob.views)
+    sh_proj = prob.layout.rest_projected
     exchange = prob.exchange if world_size > 1 else "none"
     del prob, vr, vs, ys, x, g
     torch.cuda.empty_cache()
@@ -255,7 +277,7 @@ def main():
                                    f"view(s) per GPU (BASELINE configs[2]; configs[3] at 8 GPUs)",
                        "P": args.P, "sh_degree": args.sh, "width": W, "height": H,
                        "views_total": n_views, "parallelism": f"views sharded x{world_size}",
-                       "exchange": exchange},
+                       "exchange": exchange, "sh_rest_projected": bool(sh_proj)},
             "cg_matvecs_per_s": args.steps / t_cg,
             "raster_mpix_s": mpix,
             "forward_ms_per_view": 1e3 * t_fwd / fsteps / max(n_views_local, 1),
@@ -269,6 +291,7 @@ def main():
             "lm_step": lm,
             "ssim_cg": ssim,
             "first_order": fo,
+            "cg_full_layout": cg_full,
         }
         print(json.dumps(line), flush=True)
     if world_size > 1:
@@ -334,7 +357,7 @@ def time_ssim_cg(model, cams, bg, steps=10):
     """CG iterations of the LM normal equations with the SSIM residual ([r1; r2], lambda_dssim 0.2):
     per view J v -> image-space factor (separable 11-tap SSIM JVP / VJP) -> seeded VJP -> gather."""
     from gslm.lm import LMProblem, cgls_fused
-    prob = LMProblem(model, cams, bg, ssim=True)
+    prob = LMProblem(model, cams, bg, ssim=True, sh_projection="auto")
     prob.evaluate()
     g = prob.rhs(prob.zeros())
     cgls_fused(prob, g, max_iter=2, restart_iter=2, check_every=False)

@@ -338,7 +338,19 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   }
   if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
-  const GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
+  const bool proj = opts && (opts->flags & GSLM_MV_SH_REST_PROJECTED) && b.g.M > 1;
+  GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
+  if (proj) {
+    if (vin->sh_rest && vin->sh_rest_stride != 3) {
+      set_error("matvec: a projected SH-rest group has 3 floats per Gaussian (sh_rest_stride 3)");
+      return GSLM_ERR_INVALID;
+    }
+    if (stages & GSLM_STAGE_SCREEN) {
+      set_error("matvec: GSLM_MV_SH_REST_PROJECTED is a single-view mode (no SCREEN stage)");
+      return GSLM_ERR_INVALID;
+    }
+    t.rest_proj = 1;
+  }
   XpbyK xp{};
   const bool fused_xpby = opts && opts->xpby_s;
   if (fused_xpby) {
@@ -347,9 +359,9 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
       set_error("matvec: xpby needs the TANGENT stage and beta_num / beta_den");
       return GSLM_ERR_INVALID;
     }
-    const int R = 3 * (b.g.M - 1);
+    const int R = proj ? 3 : 3 * (b.g.M - 1);
     if (vin->sh_dc_stride != 3 || sv->sh_dc_stride != 3 || (b.g.M > 1 && (vin->sh_rest_stride != R || sv->sh_rest_stride != R))) {
-      set_error("matvec: xpby needs contiguous SH groups (dc stride 3, rest stride 3(M-1))");
+      set_error("matvec: xpby needs contiguous SH groups (dc stride 3, rest stride 3(M-1), or 3 projected)");
       return GSLM_ERR_INVALID;
     }
     float* pp[6] = {vin->means3D, vin->sh_dc, vin->sh_rest, vin->scales, vin->rotations, vin->opacities};
@@ -420,10 +432,28 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   if (!(stages & GSLM_STAGE_GATHER)) return GSLM_OK;
   double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
   if ((st = launch_gather_lm(b.v, b.g, b.gb, b.sb, make_gradk(y), make_gradk(vin), damp7,
-                             (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, part, s)))
+                             (stages & GSLM_STAGE_OVERWRITE) != 0, mask_xyz != 0, part, s, proj)))
     return st;
   if (dot_out) return gslm_dot_finalize(part, (int32_t)((b.g.P + 255) / 256), dot_out, stream);
   return GSLM_OK;
+}
+
+int gslm_sh_rest_project(const gslm_view* view, const gslm_gaussians* gi, int32_t mode, const float* in,
+                         int64_t in_stride, float* out, int64_t out_stride, void* stream) {
+  ViewK v;
+  GaussK g;
+  int st;
+  if (!view || !gi) { set_error("sh_rest_project: NULL view / gaussians"); return GSLM_ERR_INVALID; }
+  if ((st = make_view(view, gi->max_coeffs, &v))) return st;
+  if ((st = make_gauss(gi, &v, &g, false))) return st;
+  if (mode != 0 && mode != 1) { set_error("sh_rest_project: mode must be 0 (expand) or 1 (project)"); return GSLM_ERR_INVALID; }
+  if (g.P > 0 && g.M > 1 && (!in || !out || !g.means3D)) { set_error("sh_rest_project: NULL buffer"); return GSLM_ERR_INVALID; }
+  const int64_t full = 3 * (int64_t)(g.M - 1);
+  if ((mode == 0 && (in_stride < 3 || out_stride < full)) || (mode == 1 && (in_stride < full || out_stride < 3))) {
+    set_error("sh_rest_project: strides too small for [P,3] / [P,M-1,3] rows");
+    return GSLM_ERR_INVALID;
+  }
+  return launch_sh_rest_project(v, g, mode, in, in_stride, out, out_stride, (hipStream_t)stream);
 }
 
 int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, const float* screen,

@@ -104,7 +104,49 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
   lm_epilogue<WANT_MEANS, true>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
 }
 
+// The SH-rest group of one view's Krylov space (GSLM_MV_SH_REST_PROJECTED): with one view every
+// Gaussian's SH-rest column of J is B_rest(dir) (x) (d rgb), so J^T J + D (D a scalar on the group) maps
+// span{B_rest(dir) (x) e_c} into itself, and every CG iterate started from J^T b stays there: 3
+// coordinates per Gaussian along the unit direction Bh = B_rest / |B_rest| replace 3(M-1) floats.
+//   mode 0 (expand):  out[i, k-1, c] = Bh_k in[i, c]         (k < nc; 0 for inactive coefficients)
+//   mode 1 (project): out[i, c] = sum_k Bh_k in[i, k-1, c]
+__global__ __launch_bounds__(256) void k_sh_rest_project(ViewK v, GaussK g, int mode, const float* __restrict__ in,
+                                                         int64_t in_stride, float* __restrict__ out,
+                                                         int64_t out_stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.P) return;
+  const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
+  const float dx = x - v.campos[0], dy = y - v.campos[1], dz = z - v.campos[2];
+  const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+  float B[16];
+  sh_basis(v.D, dx / len, dy / len, dz / len, B);
+  const int nc = (v.D + 1) * (v.D + 1);
+  const float nb = sh_rest_norm(B, nc);
+  const float inv = nb > 0.f ? 1.f / nb : 0.f;
+  if (mode == 0) {
+    for (int k = 1; k < g.M; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) out[i * out_stride + 3 * (k - 1) + c] = k < nc ? (B[k] * inv) * in[i * in_stride + c] : 0.f;
+  } else {
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int k = 1; k < g.M && k < nc; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += (B[k] * inv) * in[i * in_stride + 3 * (k - 1) + c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[i * out_stride + c] = acc[c];
+  }
+}
+
 // ---------------------------------------------------------------- launchers
+int launch_sh_rest_project(const ViewK& v, const GaussK& g, int mode, const float* in, int64_t in_stride, float* out,
+                           int64_t out_stride, hipStream_t s) {
+  if (g.P == 0 || g.M < 2) return GSLM_OK;
+  hipLaunchKernelGGL(k_sh_rest_project, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, v, g, mode, in,
+                     in_stride, out, out_stride);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, const BinBufs& bb,
                           const ScratchBufs& sb, const GradK& out, bool want_means, hipStream_t s) {
   (void)bb;
@@ -125,10 +167,10 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
 
 int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
                      const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
-                     hipStream_t s) {
+                     hipStream_t s, bool rest_proj) {
   if (g.P == 0) return GSLM_OK;
   FlatK o;
-  const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o);
+  const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o, rest_proj);
   if (st) return st;
   const unsigned nb = (unsigned)((g.P + 255) / 256);
   const size_t rest_lds = sh_stage_floats<true>(g.M) * sizeof(float);

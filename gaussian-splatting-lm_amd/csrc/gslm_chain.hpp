@@ -92,6 +92,17 @@ __device__ __forceinline__ void aa_grad(const Geo& e, float& ha, float& hb, floa
   }
 }
 
+// |B_rest(dir)|: the norm of the SH basis values of coefficients 1..nc-1 (for real orthonormal SH it is
+// sqrt(sum_{l=1..D} (2l+1) / 4 pi) at every direction; computed from the values themselves so the tangent
+// and the gather of a projected SH-rest group use the same number)
+__device__ __forceinline__ float sh_rest_norm(const float B[16], int nc) {
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 1; k < 16; ++k)
+    if (k < nc) acc += B[k] * B[k];
+  return sqrtf(acc);
+}
+
 struct ChainOut {
   float dm2[2];
   float dmean[3];
@@ -456,10 +467,21 @@ __device__ __forceinline__ void chain_jvp(const ViewK& v, const GaussK& g, const
     if (t.dc) {
       float B[16];
       sh_basis(v.D, e.dir[0], e.dir[1], e.dir[2], B);
-      for (int k = 0; k < nc; ++k) {
-        if (k > 0 && !t.rest) break;
+      if (t.rest_proj) {
+        // projected SH-rest tangent: sum_k B_k v_k = |B_rest| c for v = (B_rest / |B_rest|) (x) c
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) dres[ch] += B[k] * t.sh(i, k, ch);
+        for (int ch = 0; ch < 3; ++ch) dres[ch] += B[0] * t.sh(i, 0, ch);
+        if (t.rest && nc > 1) {
+          const float nb = sh_rest_norm(B, nc);
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) dres[ch] += nb * t.rest[(i - t.rest_base) * t.rest_stride + ch];
+        }
+      } else {
+        for (int k = 0; k < nc; ++k) {
+          if (k > 0 && !t.rest) break;
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) dres[ch] += B[k] * t.sh(i, k, ch);
+        }
       }
     }
     if (t.means3D && v.D > 0) {

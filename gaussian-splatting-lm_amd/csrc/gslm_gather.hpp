@@ -13,6 +13,7 @@ struct FlatK {
   float damp[6];
   int use_damp;
   int overwrite;
+  int rest_proj;      // GSLM_MV_SH_REST_PROJECTED: the rest group is 3 floats per Gaussian (see chain_jvp)
   double* dot_part;   // per-block partials of <v, y> over the written elements (NULL = off)
 };
 
@@ -71,9 +72,14 @@ __device__ __forceinline__ double store_group(float* y, float d, int use_damp, i
 
 // FlatK over a flat param-space output y and input v (GradK views of the 7-group vectors).
 inline int make_flatk(const GaussK& g, const GradK& y, const GradK& vin, const double* damp7, bool overwrite,
-                      double* dot_part, FlatK* out) {
-  if (g.cov3D || g.colors || !g.raw || y.rest_stride != 3 * (g.M - 1) || y.dc_stride != 3) {
+                      double* dot_part, FlatK* out, bool rest_proj = false) {
+  const int64_t R = rest_proj ? 3 : 3 * (g.M - 1);
+  if (g.cov3D || g.colors || !g.raw || (g.M > 1 && y.rest_stride != R) || y.dc_stride != 3) {
     set_error("LM gather expects raw leaves with SH colours and a flat param-space output");
+    return GSLM_ERR_INVALID;
+  }
+  if (rest_proj && g.M > 1 && vin.rest && vin.rest_stride != 3) {
+    set_error("LM gather: a projected SH-rest group has 3 floats per Gaussian in v and y");
     return GSLM_ERR_INVALID;
   }
   FlatK o;
@@ -83,6 +89,7 @@ inline int make_flatk(const GaussK& g, const GradK& y, const GradK& vin, const d
   for (int k = 0; k < 6; ++k) o.damp[k] = damp7 ? (float)damp7[k] : 0.f;
   o.use_damp = damp7 ? 1 : 0;
   o.overwrite = overwrite ? 1 : 0;
+  o.rest_proj = (rest_proj && g.M > 1) ? 1 : 0;
   o.dot_part = dot_part;
   if (o.use_damp || dot_part)
     for (int k = 0; k < 6; ++k)
@@ -115,7 +122,8 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + tid;
   const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
-  const int R = 3 * (g.M - 1);
+  // a projected SH-rest group is a 3-wide group of its own below; the LDS-staged stream covers none
+  const int R = o.rest_proj ? 0 : 3 * (g.M - 1);
   const bool dot = o.dot_part != nullptr;
   const int u = o.use_damp, ow = o.overwrite;
   const bool need_v = u || dot;
@@ -142,7 +150,15 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
     dacc += store_group<4>(o.y[4], o.damp[4], u, 4 * i, ow, dot, co.drot, vr, yr);
     const float dop[1] = {co.dop};
     dacc += store_group<1>(o.y[5], o.damp[5], u, i, ow, dot, dop, vo, yo);
-    if (FACTORED) {
+    if (o.rest_proj) {
+      // B_rest (x) dres in the coordinate along B_rest / |B_rest|: |B_rest| dres
+      float vp[3], yp[3], val[3];
+      load_group<3>(o.v[2], o.y[2], 3 * i, need_v, !ow, vp, yp);
+      const float nb = sh_rest_norm(co.shB, nc);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) val[ch] = nb * co.dres[ch];
+      dacc += store_group<3>(o.y[2], o.damp[2], u, 3 * i, ow, dot, val, vp, yp);
+    } else if (FACTORED) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) s_rest[tid * SHB_STRIDE + k] = co.shB[k];
       float* s_d = s_rest + 256 * SHB_STRIDE;

@@ -20,6 +20,9 @@ struct GaussK {
   int64_t rest_stride;
   const float* colors;
   int64_t rest_base = 0;  // rest holds Gaussians rest_base.. (an LDS-staged block slice) when nonzero
+  // tangents only (GSLM_MV_SH_REST_PROJECTED): rest holds 3 floats per Gaussian, the coordinates of the
+  // SH-rest tangent along the unit basis direction B_rest(dir) / |B_rest(dir)| of this view
+  int rest_proj = 0;
   __device__ __forceinline__ float sh(int64_t i, int k, int c) const {
     return k == 0 ? dc[i * dc_stride + c] : rest[(i - rest_base) * rest_stride + 3 * (k - 1) + c];
   }
@@ -388,5 +391,7 @@ int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, co
                          hipStream_t s);
 int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, const GradK& y,
                      const GradK& vin, const double* damp7, bool overwrite, bool mask_xyz, double* dot_part,
-                     hipStream_t s);
+                     hipStream_t s, bool rest_proj = false);
+int launch_sh_rest_project(const ViewK& v, const GaussK& g, int mode, const float* in, int64_t in_stride, float* out,
+                           int64_t out_stride, hipStream_t s);
 }  // namespace gslm

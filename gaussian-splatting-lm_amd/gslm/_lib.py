@@ -108,6 +108,9 @@ EXPORTS = {
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(GslmGrads),
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_sh_rest_project": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                            ctypes.c_void_p]),
     "gslm_gather_screen": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
                                           ctypes.c_void_p, ctypes.POINTER(GslmGrads), ctypes.POINTER(GslmGrads),
                                           ctypes.c_void_p, ctypes.c_void_p]),

@@ -28,6 +28,7 @@ from gslm.params import GROUPS, ParamLayout, raw_gaussians
 STAGE_ALL = 7
 STAGE_OVERWRITE = 8
 MV_TAIL_CLEAN = 1  # gslm_matvec_opts.flags: GSLM_MV_TAIL_CLEAN
+MV_SH_REST_PROJECTED = 2  # GSLM_MV_SH_REST_PROJECTED
 
 DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling": 5e-2, "rotation": 5e-2,
                 "opacity": 5e-2, "exposure": 1e1}
@@ -77,9 +78,14 @@ class LMProblem:
     """The LM normal equations of one camera batch (one LM step's worth of cached geometry)."""
 
     def __init__(self, model, cams, bg, gts=None, alpha_masks=None, mask_xyz=True, damp=None, device="cuda",
-                 ssim=False, lambda_dssim=0.2):
+                 ssim=False, lambda_dssim=0.2, sh_projection=False):
         """ssim=False: the residual train_jvp.py uses (disable_ssim=True, [r; r]); ssim=True: the
-        [r1; r2] residual with the SSIM term (batch_training_loss.py:18-30, gslm_ssim_*)."""
+        [r1; r2] residual with the SSIM term (batch_training_loss.py:18-30, gslm_ssim_*).
+
+        sh_projection: param-space vectors carry the SH-rest group as 3 coordinates per Gaussian along the
+        view's unit basis direction (GSLM_MV_SH_REST_PROJECTED; one view only -- with one view the CG
+        iterates of (J^T J + D) x = J^T b never leave that span).  True / False / "auto" (= one camera and
+        SH degree > 0).  `expand` / `project` convert to and from the reference's layout (`full_layout`)."""
         self.model = model
         self.ssim, self.lambda_dssim = bool(ssim), float(lambda_dssim)
         if self.ssim and not mask_xyz:
@@ -90,7 +96,13 @@ class LMProblem:
         self.mask_xyz = bool(mask_xyz)
         P = model._xyz.shape[0]
         K = 1 + model._features_rest.shape[1]
-        self.layout = ParamLayout(P, K, model._exposure.shape[0])
+        if sh_projection == "auto":
+            sh_projection = len(cams) == 1 and K > 1 and model.active_sh_degree > 0
+        if sh_projection and len(cams) != 1:
+            raise ValueError("sh_projection is a single-view mode (the Krylov space of one view's J)")
+        self.full_layout = ParamLayout(P, K, model._exposure.shape[0])
+        self.layout = ParamLayout(P, K, model._exposure.shape[0], rest_projected=bool(sh_projection))
+        self.mv_flags = MV_SH_REST_PROJECTED if self.layout.rest_projected else 0
         self.damp = DEFAULT_DAMP if damp is None else damp
         self._bounds, self._damps = self.layout.group_damp_arrays(self.damp)
         self.gts = [c.original_image.to(device) for c in cams] if gts is None else gts
@@ -165,7 +177,7 @@ class LMProblem:
             for b, vr in enumerate(self.views):
                 opts = _lib.GslmMatvecOpts()
                 opts.stages = 2 | 4 | (STAGE_OVERWRITE if b == 0 else 0)  # RENDER | GATHER
-                opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
+                opts.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
                 opts.pixel_seed = self.seeds[b].data_ptr()
                 check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(ys),
                                               self.seeds[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
@@ -177,19 +189,67 @@ class LMProblem:
             e0, e1 = self.layout.offsets["exposure"]
             out[e0:e1].zero_()
             return out
+        if self.layout.rest_projected:
+            full = torch.zeros(self.full_layout.numel, dtype=torch.float32, device=self.device)
+            self.rhs_full(full)
+            return self.project(full, out)
+        return self.rhs_full(out)
+
+    def rhs_full(self, out):
+        """J^T b through the drop-in gslm_backward, in the reference's layout (full_layout)."""
+        g = raw_gaussians(self.model)
         out.zero_()
-        grads = self.layout.grads_struct(out, accumulate=True)
+        grads = self.full_layout.grads_struct(out, accumulate=True)
         for b, vr in enumerate(self.views):
             dL = self.seeds[b]  # -2 m 1[0 <= R <= 1] r, from gslm_lm_residual
             check(lib.gslm_backward(ctypes.byref(vr.view), ctypes.byref(g), vr.geom.data_ptr(), vr.binning.data_ptr(),
                                     vr.N, vr.image.data_ptr(), dL.data_ptr(), None, vr.scratch.data_ptr(),
                                     vr.scratch.numel(), ctypes.byref(grads), self.stream), "gslm_backward")
             vr.tail_clean = False
-        self._apply_mask(out)
+        self._apply_mask(out, self.full_layout)
         return out
 
-    def _apply_mask(self, vec):
-        o = self.layout.offsets
+    # -------------------------------------------------------------- SH-rest projection (sh_projection)
+    def _rest_convert(self, mode, src, dst, src_layout, dst_layout):
+        if self.layout.K < 2:
+            return
+        g = raw_gaussians(self.model)
+        a0 = src_layout.offsets["features_rest"][0]
+        b0 = dst_layout.offsets["features_rest"][0]
+        src_w = 3 * src_layout.shapes["features_rest"][1]
+        dst_w = 3 * dst_layout.shapes["features_rest"][1]
+        check(lib.gslm_sh_rest_project(ctypes.byref(self.views[0].view), ctypes.byref(g), mode,
+                                       src.data_ptr() + 4 * a0, src_w, dst.data_ptr() + 4 * b0, dst_w, self.stream),
+              "gslm_sh_rest_project")
+
+    def _copy_other_groups(self, src, dst, src_layout, dst_layout):
+        for name in GROUPS:
+            if name == "features_rest":
+                continue
+            a0, a1 = src_layout.offsets[name]
+            b0, b1 = dst_layout.offsets[name]
+            dst[b0:b1].copy_(src[a0:a1])
+
+    def expand(self, x, out=None):
+        """A vector of this problem's layout in the reference's (full_layout); x itself when not projected."""
+        if not self.layout.rest_projected:
+            return x
+        out = torch.empty(self.full_layout.numel, dtype=torch.float32, device=x.device) if out is None else out
+        self._copy_other_groups(x, out, self.layout, self.full_layout)
+        self._rest_convert(0, x, out, self.layout, self.full_layout)
+        return out
+
+    def project(self, x_full, out=None):
+        """full_layout -> this problem's layout (the orthogonal projection onto the view's SH-rest span)."""
+        if not self.layout.rest_projected:
+            return x_full if out is None else out.copy_(x_full)
+        out = torch.empty(self.layout.numel, dtype=torch.float32, device=x_full.device) if out is None else out
+        self._copy_other_groups(x_full, out, self.full_layout, self.layout)
+        self._rest_convert(1, x_full, out, self.full_layout, self.layout)
+        return out
+
+    def _apply_mask(self, vec, layout=None):
+        o = (layout or self.layout).offsets
         if self.mask_xyz:
             vec[o["xyz"][0]:o["xyz"][1]].zero_()
         vec[o["exposure"][0]:o["exposure"][1]].zero_()
@@ -228,7 +288,7 @@ class LMProblem:
         for b, vr in enumerate(self.views):
             opts = _lib.GslmMatvecOpts()
             opts.stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
-            opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
+            opts.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
             opts.damp7 = self._damps if (damp and b == 0) else None
             if pre is not None and b == 0:
                 ss = self._pre_opts(opts, v, pre)  # noqa: F841  (kept alive for the call)
@@ -283,6 +343,7 @@ class LMProblem:
         jv, u = self._jv[b], self._u[b]
         o1 = _lib.GslmMatvecOpts()
         o1.stages = 1 | 2  # TANGENT | RENDER
+        o1.flags = self.mv_flags
         o1.jv_out = jv.data_ptr()
         o1.xpby_s, o1.beta_num, o1.beta_den = opts.xpby_s, opts.beta_num, opts.beta_den
         o1.xpby_tail_v, o1.xpby_tail_s, o1.xpby_tail_n = opts.xpby_tail_v, opts.xpby_tail_s, opts.xpby_tail_n
@@ -295,7 +356,7 @@ class LMProblem:
                                    u.data_ptr(), self.stream), "gslm_ssim_normal")
         o2 = _lib.GslmMatvecOpts()
         o2.stages = 2 | 4 | (opts.stages & STAGE_OVERWRITE)  # RENDER | GATHER
-        o2.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
+        o2.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
         o2.pixel_seed = u.data_ptr()
         o2.damp7 = opts.damp7
         o2.dot_vy, o2.dot_scratch, o2.dot_scratch_bytes = opts.dot_vy, opts.dot_scratch, opts.dot_scratch_bytes
@@ -492,24 +553,26 @@ def update_params(model, layout, step, scale):
 
 
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
-            verbose=False, device="cuda"):
-    """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search."""
-    prob = LMProblem(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
+            verbose=False, device="cuda", sh_projection="auto"):
+    """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search.
+    With one training view the SH-rest group of the CG vectors is carried projected (LMProblem)."""
+    prob = LMProblem(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device, sh_projection=sh_projection)
     start_loss = prob.evaluate()
     g = prob.rhs(prob.zeros())
     s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
                          verbose=verbose)
+    s = prob.expand(s)
     val = LMProblem(model, val_cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
     alpha = 2.0
     best_alpha, best_loss = alpha, math.inf
-    update_params(model, prob.layout, s, alpha)
+    update_params(model, prob.full_layout, s, alpha)
     for _ in range(6):
         vl = float(val.evaluate())
         if vl < best_loss:
             best_loss, best_alpha = vl, alpha
         new_alpha = alpha * 0.5
-        update_params(model, prob.layout, s, new_alpha - alpha)
+        update_params(model, prob.full_layout, s, new_alpha - alpha)
         alpha = new_alpha
-    update_params(model, prob.layout, s, best_alpha - alpha)
+    update_params(model, prob.full_layout, s, best_alpha - alpha)
     final = float(val.evaluate())
     return dict(start_loss=float(start_loss), final_val_loss=final, best_alpha=best_alpha, cg=info, step=s)

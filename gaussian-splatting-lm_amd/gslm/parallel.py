@@ -144,4 +144,6 @@ def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto"
     """LMProblem over this rank's views, wrapped for the cross-rank reductions.  all_cams (every
     rank's views, in rank order) enables the screen exchange."""
     from gslm.lm import LMProblem
+    if world()[1] > 1 or (all_cams is not None and len(all_cams) > 1):
+        kw["sh_projection"] = False  # the SH-rest span is one view's: the global batch has several
     return ShardedOperator(LMProblem(model, cams, bg, **kw), group=group, all_cams=all_cams, exchange=exchange)

@@ -164,6 +164,13 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
  * re-deriving each sorted entry's row slot (kept in the binning buffer's free sort ping-pong half).
  * Both depend on the geometry only, so an LM step's CG loop pays for them once. */
 #define GSLM_MV_TAIL_CLEAN 1
+/* opts->flags: GSLM_MV_SH_REST_PROJECTED -- single-view Krylov space of the SH-rest group.  With one view,
+ * Gaussian i's SH-rest columns of J are B_rest(dir_i) (x) d rgb, so J^T W J + D (D a scalar on the group)
+ * maps span{B_rest(dir_i) (x) e_c} to itself and every CG iterate started from J^T b lies in it.  With this
+ * flag the SH-rest group of v, y and xpby_s holds 3 floats per Gaussian (sh_rest_stride 3): the coordinates
+ * along Bh = B_rest / |B_rest| (the same operator on the 3(M-1) -> 3 coordinates of that span; convert with
+ * gslm_sh_rest_project).  Not for the SCREEN stage (multi-view). */
+#define GSLM_MV_SH_REST_PROJECTED 2
 typedef struct gslm_matvec_opts {
   int32_t stages;         /* GSLM_STAGE_* bits; 0 means GSLM_STAGE_ALL (accumulate) */
   int32_t flags;          /* GSLM_MV_* bits */
@@ -206,6 +213,13 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gs
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                         int64_t num_rendered, const void* image, void* scratch, size_t scratch_bytes,
                         const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
+
+/* SH-rest coordinates of GSLM_MV_SH_REST_PROJECTED for this view (gaussians: the raw leaves; means3D and
+ * max_coeffs are used).  mode 0 (expand): out[i*out_stride + 3(k-1) + c] = Bh_k(dir_i) in[i*in_stride + c];
+ * mode 1 (project): out[i*out_stride + c] = sum_k Bh_k(dir_i) in[i*in_stride + 3(k-1) + c]; Bh = B_rest/|B_rest|
+ * over the view's active degree (inactive coefficients expand to 0). */
+int gslm_sh_rest_project(const gslm_view* view, const gslm_gaussians* g, int32_t mode, const float* in,
+                         int64_t in_stride, float* out, int64_t out_stride, void* stream);
 
 /* ---- view-sharded exchange (multi-GPU LM product), SURVEY 8(e) ----
  * Instead of all-reducing the param-space partial J^T W J v (F = 59 floats per Gaussian at SH 3),

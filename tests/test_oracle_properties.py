@@ -85,3 +85,51 @@ def test_empty_and_culled_inputs():
     c, r, d = tr.rasterize(behind["means3D"], torch.zeros_like(behind["means3D"]), behind["opacities"], st,
                            shs=behind["shs"], scales=behind["scales"], rotations=behind["rotations"])
     assert (r == 0).all() and (d == 0).all()
+
+
+def _rest_basis(model, cam):
+    """Unit SH-rest basis directions Bh_i = B_rest(dir_i) / |B_rest(dir_i)| [P, K-1] (utils/sh_utils.py basis)."""
+    D = model.active_sh_degree
+    K = (D + 1) ** 2
+    d = model._xyz.detach().double() - cam.camera_center.double()
+    d = d / d.norm(dim=1, keepdim=True)
+    eye = torch.eye(K, dtype=torch.float64).expand(d.shape[0], 1, K, K)[:, 0]  # [P, K, K]: coefficient k = e_k
+    B = torch.stack([tr.eval_sh(D, eye[:, :, k:k + 1].expand(-1, -1, 3), d)[:, 0] for k in range(K)], 1)  # [P, K]
+    Br = B[:, 1:]
+    return Br / Br.norm(dim=1, keepdim=True)
+
+
+@pytest.mark.parametrize("ssim", [False, True])
+def test_single_view_krylov_space_keeps_sh_rest_in_basis_span(ssim):
+    """The claim behind GSLM_MV_SH_REST_PROJECTED: with one view, J^T b and (J^T J + D) applied to any
+    vector whose SH-rest rows are Bh_i (x) c_i keep the SH-rest rows in span{Bh_i (x) e_c}, so CG from
+    x0 = 0 never leaves it (checked on the oracle's autograd / forward-AD operator, float32)."""
+    from oracle.lm_ref import OracleLMProblem
+    model, cams = make_scene("tiny_300_sh2_40x33")
+    cam = cams[0]
+    cam.original_image = torch.rand(3, cam.image_height, cam.image_width, generator=torch.Generator().manual_seed(3))
+    op = OracleLMProblem(model, [cam], torch.zeros(3), ssim=ssim)
+    op.evaluate()
+    Bh = _rest_basis(model, cam).float()  # [P, K-1]
+    a, b = op.layout.offsets["features_rest"]
+    P, Km1 = Bh.shape
+
+    def off_span(vec):
+        R = vec[a:b].view(P, Km1, 3)
+        coef = (Bh[:, :, None] * R).sum(1)  # [P, 3]
+        resid = R - Bh[:, :, None] * coef[:, None, :]
+        return float(resid.abs().max()), float(R.abs().max())
+
+    g = op.rhs()
+    r, scale = off_span(g)
+    assert scale > 0 and r <= 1e-5 * scale
+    y = op.zeros()
+    op.matvec(g, y)
+    r, scale = off_span(y)
+    assert scale > 0 and r <= 1e-5 * scale
+    # and a generic vector of the span (random coefficients in every group)
+    v = torch.randn(op.layout.numel, generator=torch.Generator().manual_seed(4))
+    v[a:b] = (Bh[:, :, None] * torch.randn(P, 1, 3, generator=torch.Generator().manual_seed(5))).reshape(-1)
+    op.matvec(v, y)
+    r, scale = off_span(y)
+    assert r <= 1e-5 * scale
