@@ -95,3 +95,28 @@ def test_projected_lm_step_matches_full():
     assert abs(a["final_val_loss"] - b["final_val_loss"]) <= 1e-4 * a["final_val_loss"]
     for t1, t2 in zip(m.params(), m2.params()):
         assert _close(t2.detach(), t1.detach(), 1e-4)
+
+
+def test_projected_and_full_cgls_against_float64_oracle():
+    """Both float32 GPU layouts against the float64 oracle CGLS of the same single-view problem: the
+    projected solution is as accurate as the full one (rel 2e-3 in norm, the reference-schedule bar)."""
+    from gslm.lm import cgls_fused
+    from oracle.lm_ref import OracleLMProblem, cgls_ref
+    m, cam, pf, pp = _one_view(False)
+    mc = copy.deepcopy(m).to("cpu")
+    for t in mc.params():
+        t.data = t.data.double()
+    cc = copy.deepcopy(cam).to("cpu")
+    for k in ("original_image", "alpha_mask", "world_view_transform", "projection_matrix", "full_proj_transform",
+              "camera_center"):
+        setattr(cc, k, getattr(cc, k).double())
+    op = OracleLMProblem(mc, [cc], torch.zeros(3, dtype=torch.float64))
+    op.evaluate()
+    x64 = cgls_ref(op, op.rhs(), 10, 10)
+    errs = {}
+    for name, p in (("full", pf), ("proj", pp)):
+        p.evaluate()
+        x, _ = cgls_fused(p, p.rhs(p.zeros()), max_iter=10, restart_iter=10, check_every=True)
+        errs[name] = float((p.expand(x).double().cpu() - x64).norm() / x64.norm())
+    assert errs["full"] < 2e-3 and errs["proj"] < 2e-3, errs
+    assert errs["proj"] <= 2 * errs["full"] + 1e-4, errs
