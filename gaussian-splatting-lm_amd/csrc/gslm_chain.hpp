@@ -135,6 +135,9 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
     co.dsh[k][0] = co.dsh[k][1] = co.dsh[k][2] = 0.f;
     co.shB[k] = 0.f;
   }
+  // the factored SH epilogues stage shB x dres for every Gaussian, culled ones included (0 x garbage
+  // would be NaN when the register happens to hold one)
+  co.dres[0] = co.dres[1] = co.dres[2] = 0.f;
   if (!visible) return;
   Geo e;
   compute_geo<RAW>(v, g, i, clamped, e);

@@ -142,6 +142,7 @@ struct VjpPix {
   // itself is carried: accd = <acc, dL/dpix> (+ acc_inv dL/dinvdepth), last_cd = the previous
   // Gaussian's <colour, dL/dpix> (+ invdepth term).
   float accd, last_alpha, last_cd;
+  float tb;         // -T_final <bg, dL/dpix>: the background term of dL/dalpha is tb / (1 - alpha)
 };
 
 __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside, float T_final, uint32_t last,
@@ -152,6 +153,7 @@ __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside,
   s.dpix[0] = d0; s.dpix[1] = d1; s.dpix[2] = d2;
   s.dinv = dinv;
   s.bg_dot = (v.bg[0] * d0 + v.bg[1] * d1) + v.bg[2] * d2;
+  s.tb = -s.T_final * s.bg_dot;
   s.accd = 0.f;
   s.last_alpha = 0.f;
   s.last_cd = 0.f;
@@ -229,6 +231,10 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     for (int j = it.next(); j >= 0; j = it.next()) {
       const float4 a = s_r0[j], b = s_r1[j];
       const float2 c = s_r2[j];
+      // the whole record in one LDS round trip at the top of the iteration (the empty asm pins the loads
+      // here; otherwise the colour half is fetched after the alpha test, a second exposed LDS latency;
+      // prefetching the next hit's record instead measured 9% slower: it costs issue slots, not latency)
+      asm volatile("" : : "v"(b.z), "v"(b.w), "v"(c.x), "v"(c.y));
       {
         const uint32_t contributor = (uint32_t)(base - j);  // 0-based list position
         const float dx = a.x - pxf, dy = a.y - pyf;
@@ -236,11 +242,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
         const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
-        // <colour, dL/dpix> for every lane, so the record's colour is read with the rest of it (one LDS
-        // round trip per entry instead of a second one inside the valid branch)
-        // the record's colour (and inverse depth) read with the rest of it: one LDS round trip per entry
-        // instead of a second one inside the valid branch (the empty asm pins the loads here)
-        asm volatile("" : : "v"(b.z), "v"(b.w), "v"(c.x), "v"(c.y));
+        // <colour, dL/dpix> for every lane (the colour is already in registers)
         float cd;
         {
 #pragma clang fp contract(fast)
@@ -262,19 +264,21 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
 #pragma unroll
           for (int ch = 0; ch < 3; ++ch) gv[6 + ch] = dchannel * st.dpix[ch];
           if (WITH_INV) gv[9] = dchannel * st.dinv;
-          float dL_dalpha = (cd - st.accd) * st.T;
+          // dL/dalpha = (<c, u> - acc) T - T_final / (1 - alpha) <bg, u>   (tb = -T_final <bg, u>)
+          const float dL_dalpha = (cd - st.accd) * st.T + st.tb * inv1ma;
           st.last_alpha = alpha;
-          dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
-          const float dL_dG = b.y * dL_dalpha;
-          const float gdx = G * dx, gdy = G * dy;
-          if (WITH_XY) {
-            gv[0] = dL_dG * (-gdx * a.z - gdy * a.w);
-            gv[1] = dL_dG * (-gdy * b.x - gdx * a.w);
-          }
-          gv[2] = -0.5f * gdx * dx * dL_dG;
-          gv[3] = -gdx * dy * dL_dG;
-          gv[4] = -0.5f * gdy * dy * dL_dG;
           gv[5] = G * dL_dalpha;
+          // h = G dL/dG with G = exp(power): dL/dpower = h; the conic rows carry h dx^2, h dx dy, h dy^2
+          // and their constant factors (-1/2, -1, -1/2) are applied once per row at the combine
+          const float h = b.y * gv[5];
+          const float hdx = h * dx, hdy = h * dy;
+          if (WITH_XY) {
+            gv[0] = -(hdx * a.z + hdy * a.w);
+            gv[1] = -(hdy * b.x + hdx * a.w);
+          }
+          gv[2] = hdx * dx;
+          gv[3] = hdx * dy;
+          gv[4] = hdy * dy;
         }
         const bool any = __ballot(valid) != 0ull;
 #ifdef GSLM_EXPERIMENT_COUNT
@@ -343,6 +347,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           t[q] = ((p0 + p1) + p2) + p3;
         }
       }
+      t[2] *= -0.5f;  // the conic rows' constant factors (see the hit loop)
+      t[3] = -t[3];
+      t[4] *= -0.5f;
       store_row<ROWF4>(rows, my_slot, t);
     }
   }

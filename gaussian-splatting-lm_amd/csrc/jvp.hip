@@ -18,32 +18,37 @@ struct JvpPix {
 };
 
 // Front-to-back tangent pass over the tile, BATCH list entries staged in LDS per round.
-// Block-uniform; blockDim = 256.  Wave w visits only the
-// batch elements whose alpha region reaches its 8x8 quadrant (publish_quad_masks); the stop decision is
-// frozen at the primal (`last` = n_contrib).
+// Block-uniform; blockDim = 256.  Wave w visits only the batch elements whose alpha region reaches its
+// 8x8 quadrant (publish_quad_masks) and that lie before the last position any of its pixels blends (the
+// primal's n_contrib; the same per-wave bound as vjp_tile); a lane blends entry `pos` only while
+// pos < its own n_contrib -- the stop decision frozen at the primal, without a per-iteration done flag.
 template <bool WITH_XY, bool WITH_INV, int BATCH>
 __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint32_t last, uint2 range, const uint32_t* __restrict__ point_list,
                                          const float4* __restrict__ rec, const float4* __restrict__ trec,
                                          float4* s_r0, float4* s_r1, float2* s_r2, float4* s_t0, float4* s_t1,
                                          float2* s_t2, uint64_t* s_bits, int* s_cnt) {
-  const int tid = threadIdx.x, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   o.T = 1.f;
   o.dT = 0.f;
   o.dC[0] = o.dC[1] = o.dC[2] = 0.f;
   o.dD = 0.f;
-  bool done = !inside || last == 0;
-  const int n = (int)(range.y - range.x);
-  const int rounds = (n + BATCH - 1) / BATCH;
+  const uint32_t my_last = inside ? last : 0u;
+  const int wmax = wave_max_u((int)my_last);
+  if (lane == 0) s_cnt[w] = wmax;
+  __syncthreads();
+  const int wm0 = s_cnt[0], wm1 = s_cnt[1], wm2 = s_cnt[2], wm3 = s_cnt[3];
+  const int n_eff = min(max(max(wm0, wm1), max(wm2, wm3)), (int)(range.y - range.x));
+  const int rounds = (n_eff + BATCH - 1) / BATCH;
   for (int r = 0; r < rounds; ++r) {
-    const int num_done = block_count(done, s_cnt);
-    if (num_done == TILE_PIX) break;
+    __syncthreads();  // the previous batch has been consumed
     const int k = r * BATCH + tid;
     uint32_t m = 0u;
-    if (tid < BATCH && k < n) {
+    if (tid < BATCH && k < n_eff) {
       const uint32_t e = point_list[range.x + k];
       const int64_t g = pl_id(e);
-      m = pl_mask(e);
+      // quadrants it can touch, and only the waves that still blend at this list position
+      m = pl_mask(e) & ((k < wm0 ? 1u : 0u) | (k < wm1 ? 2u : 0u) | (k < wm2 ? 4u : 0u) | (k < wm3 ? 8u : 0u));
       s_r0[tid] = rec[3 * g + 0];
       s_r1[tid] = rec[3 * g + 1];
       const float4 r2 = rec[3 * g + 2];
@@ -55,49 +60,47 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
     }
     publish_quad_masks(m, s_bits);
     __syncthreads();
-    // this wave's hits in list order, while any of its pixels is still live (latency is hidden by
-    // occupancy -- 8 waves per SIMD -- rather than by register prefetch, which costs the occupancy)
+    // this wave's hits in list order (latency is hidden by occupancy -- 8 waves per SIMD -- rather than
+    // by register prefetch, which costs issue slots and occupancy)
     HitIter it(s_bits, w);
-    for (int j = __ballot(!done) != 0ull ? it.next() : -1; j >= 0; j = __ballot(!done) != 0ull ? it.next() : -1) {
+    for (int j = it.next(); j >= 0; j = it.next()) {
       const float4 a = s_r0[j], b = s_r1[j], t0 = s_t0[j], t1 = s_t1[j];
       const float2 cc = s_r2[j], t2 = s_t2[j];
       // all of the entry's primal and tangent record in one LDS round trip (the empty asm pins the
       // loads here; otherwise the tangent half is fetched inside the branch, a second exposed latency)
       asm volatile("" : : "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w), "v"(t2.x), "v"(b.z),
                    "v"(b.w), "v"(cc.x));
-      if (!done) {
-        const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-        const float G = gexp(power);
-        const float alpha = fminf(0.99f, b.y * G);
+      const uint32_t pos = (uint32_t)(r * BATCH + j);
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float G = gexp(power);
+      const float alpha = fminf(0.99f, b.y * G);
 #ifdef GSLM_EXPERIMENT_COUNT
-        {
-          const uint64_t vb = __ballot(!(power > 0.0f) && alpha >= 1.0f / 255.0f);
-          if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&g_dbg[0], 1ull);
-            atomicAdd(&g_dbg[1], (unsigned long long)__popcll(vb));
-          }
+      {
+        const uint64_t vb = __ballot(pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f);
+        if ((threadIdx.x & 63) == 0) {
+          atomicAdd(&g_dbg[0], 1ull);
+          atomicAdd(&g_dbg[1], (unsigned long long)__popcll(vb));
         }
+      }
 #endif
-        if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-          // the tangent arithmetic decides nothing (stop is frozen at the primal): FMA-contracted
+      if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+        // the tangent arithmetic decides nothing (stop is frozen at the primal): FMA-contracted
 #pragma clang fp contract(fast)
-          float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
-          if (WITH_XY) {
-            const float ddx = t0.x, ddy = t0.y;
-            dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
-          }
-          const float dalpha = G * (t1.y + b.y * dpower);
-          const float wt = alpha * o.T;
-          const float dw = dalpha * o.T + alpha * o.dT;
-          o.dC[0] += t1.z * wt + b.z * dw;
-          o.dC[1] += t1.w * wt + b.w * dw;
-          o.dC[2] += t2.x * wt + cc.x * dw;
-          if (WITH_INV) o.dD += t2.y * wt + cc.y * dw;
-          o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
-          o.T = o.T * (1.f - alpha);
-          if ((uint32_t)(k - tid + j + 1) == last) done = true;
+        float dpower = -0.5f * (t0.z * dx * dx + t1.x * dy * dy) - t0.w * dx * dy;
+        if (WITH_XY) {
+          const float ddx = t0.x, ddy = t0.y;
+          dpower += -(a.z * dx * ddx + b.x * dy * ddy) - a.w * (ddx * dy + dx * ddy);
         }
+        const float dalpha = G * (t1.y + b.y * dpower);
+        const float wt = alpha * o.T;
+        const float dw = dalpha * o.T + alpha * o.dT;
+        o.dC[0] += t1.z * wt + b.z * dw;
+        o.dC[1] += t1.w * wt + b.w * dw;
+        o.dC[2] += t2.x * wt + cc.x * dw;
+        if (WITH_INV) o.dD += t2.y * wt + cc.y * dw;
+        o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
+        o.T = o.T * (1.f - alpha);
       }
     }
   }

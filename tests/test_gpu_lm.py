@@ -221,3 +221,28 @@ def test_fused_rhs_matches_dropin_backward():
     fresh = LMProblem(m, cams, torch.zeros(3))
     fresh.evaluate()
     assert torch.equal(y, fresh.matvec(v, fresh.zeros()))
+
+
+def test_culled_gaussians_get_exact_zero_rows():
+    """Gaussians the forward culls (radii 0: behind the camera) have exactly zero J^T b and (J^T J) v rows
+    in every group -- the SH epilogue stages them too (a NaN there once came from an unset register)."""
+    from gslm.lm import LMProblem
+    d, m, cams = _load()
+    P = m._xyz.shape[0]
+    behind = cams[0].camera_center.cuda() * 1.5  # past the camera, looking away from the scene
+    with torch.no_grad():
+        xyz = m._xyz.detach().clone()
+        xyz[::3] = behind + 0.01 * torch.randn_like(xyz[::3])
+    m.set_params(xyz, m._features_dc, m._features_rest, m._scaling, m._rotation, m._opacity, m._exposure)
+    for proj in (False, True):
+        prob = LMProblem(m, cams[:1], torch.zeros(3), sh_projection=proj)
+        prob.evaluate()
+        culled = prob.views[0].radii == 0
+        assert int(culled.sum()) >= P // 3
+        g = prob.rhs(prob.zeros())
+        v = torch.randn(prob.layout.numel, device="cuda")
+        y = prob.matvec(v, prob.zeros())
+        assert torch.isfinite(g).all() and torch.isfinite(y).all()
+        views = prob.layout.views(g)
+        for name in ("features_dc", "features_rest", "scaling", "rotation", "opacity"):
+            assert float(views[name][culled].abs().max()) == 0.0, name
