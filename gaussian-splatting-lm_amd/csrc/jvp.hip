@@ -28,6 +28,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
                                          const float4* __restrict__ rec, const float4* __restrict__ trec,
                                          float4* s_r0, float4* s_r1, float2* s_r2, float4* s_t0, float4* s_t1,
                                          float2* s_t2, uint64_t* s_bits, int* s_cnt) {
+  constexpr bool PACKED = !WITH_XY && !WITH_INV;  // the LM product's records (see the staging below)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   o.T = 1.f;
   o.dT = 0.f;
@@ -52,17 +53,49 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
       s_r0[tid] = rec[3 * g + 0];
       s_r1[tid] = rec[3 * g + 1];
       const float4 r2 = rec[3 * g + 2];
-      s_r2[tid] = make_float2(r2.x, r2.y);
-      s_t0[tid] = trec[3 * g + 0];
-      s_t1[tid] = trec[3 * g + 1];
-      const float4 t2 = trec[3 * g + 2];
-      s_t2[tid] = make_float2(t2.x, t2.y);
+      const float4 t0 = trec[3 * g + 0], t1 = trec[3 * g + 1], t2 = trec[3 * g + 2];
+      if (PACKED) {
+        // the LM product's 9 primal + 7 tangent floats as 4 float4 at one LDS stride: the hit loop reads
+        // them with one address register; the tangent conic carries its power factors (-1/2, -1, -1/2)
+        s_t0[tid] = make_float4(r2.x, -0.5f * t0.z, -t0.w, -0.5f * t1.x);  // blue, da', db', dc'
+        s_t1[tid] = make_float4(t1.y, t1.z, t1.w, t2.x);                    // dopacity, dr, dg, db
+      } else {
+        s_r2[tid] = make_float2(r2.x, r2.y);
+        s_t0[tid] = t0;
+        s_t1[tid] = t1;
+        s_t2[tid] = make_float2(t2.x, t2.y);
+      }
     }
     publish_quad_masks(m, s_bits);
     __syncthreads();
     // this wave's hits in list order (latency is hidden by occupancy -- 8 waves per SIMD -- rather than
     // by register prefetch, which costs issue slots and occupancy)
     HitIter it(s_bits, w);
+    if constexpr (PACKED) {
+      for (int j = it.next(); j >= 0; j = it.next()) {
+        const float4 a = s_r0[j], b = s_r1[j], C = s_t0[j], D = s_t1[j];
+        asm volatile("" : : "v"(b.z), "v"(b.w), "v"(C.x), "v"(C.y), "v"(C.z), "v"(C.w), "v"(D.x), "v"(D.y), "v"(D.z),
+                     "v"(D.w));
+        const uint32_t pos = (uint32_t)(r * BATCH + j);
+        const float dx = a.x - pxf, dy = a.y - pyf;
+        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float G = gexp(power);
+        const float alpha = fminf(0.99f, b.y * G);
+        if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+#pragma clang fp contract(fast)
+          const float dpower = (C.y * dx * dx + C.w * dy * dy) + C.z * dx * dy;
+          const float dalpha = G * (D.x + b.y * dpower);
+          const float wt = alpha * o.T;
+          const float dw = dalpha * o.T + alpha * o.dT;
+          o.dC[0] += D.y * wt + b.z * dw;
+          o.dC[1] += D.z * wt + b.w * dw;
+          o.dC[2] += D.w * wt + C.x * dw;
+          o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
+          o.T = o.T * (1.f - alpha);
+        }
+      }
+      continue;
+    }
     for (int j = it.next(); j >= 0; j = it.next()) {
       const float4 a = s_r0[j], b = s_r1[j], t0 = s_t0[j], t1 = s_t1[j];
       const float2 cc = s_r2[j], t2 = s_t2[j];
