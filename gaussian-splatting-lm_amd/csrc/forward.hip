@@ -15,12 +15,28 @@
 
 namespace gslm {
 
-template <bool RAW>
+// STAGE: the block's SH-rest rows (3(M-1) floats per Gaussian, contiguous: the GaussianModel leaf) are
+// staged through LDS with coalesced float4 loads first -- per-thread reads at a 180-B stride made every
+// load instruction touch 64 cache lines (k_preprocess ran at ~2.2 TB/s).
+template <bool RAW, bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* __restrict__ rec,
                                                      uint32_t* __restrict__ depth_key,
                                                      uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
                                                      int* __restrict__ radii_out) {
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];  // STAGE: [256 * rest_stride]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (STAGE) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+    const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+    const int64_t total = nv * g.rest_stride;  // floats; i0 * rest_stride * 4 B is 16-B aligned (i0 % 256 == 0)
+    const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+    float4* dst4 = reinterpret_cast<float4*>(s_sh);
+    for (int64_t e = threadIdx.x; e < total / 4; e += blockDim.x) dst4[e] = src4[e];
+    for (int64_t e = (total / 4) * 4 + threadIdx.x; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+    __syncthreads();
+    g.rest = s_sh;
+    g.rest_base = i0;
+  }
   if (i >= g.P) return;
   tiles[i] = 0u;
   depth_key[i] = 0xFFFFFFFFu;
@@ -223,12 +239,22 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   const int nb = (int)((g.P + 255) / 256);
-  if (g.raw)
-    hipLaunchKernelGGL(k_preprocess<true>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles, gb.rect,
-                       radii_out);
+  // stage the SH rest through LDS when it is the contiguous [P, M-1, 3] leaf (raw GaussianModel tensors)
+  const bool stage = !g.colors && g.rest && g.M > 1 && g.rest_stride == 3 * (g.M - 1) &&
+                     ((uintptr_t)g.rest & 15u) == 0;
+  const size_t lds = stage ? (size_t)256 * g.rest_stride * sizeof(float) : 0;
+  if (g.raw && stage)
+    hipLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, radii_out);
+  else if (g.raw)
+    hipLaunchKernelGGL((k_preprocess<true, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, radii_out);
+  else if (stage)
+    hipLaunchKernelGGL((k_preprocess<false, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, radii_out);
   else
-    hipLaunchKernelGGL(k_preprocess<false>, dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles, gb.rect,
-                       radii_out);
+    hipLaunchKernelGGL((k_preprocess<false, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, radii_out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

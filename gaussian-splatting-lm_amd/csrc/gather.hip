@@ -113,27 +113,48 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
 __global__ __launch_bounds__(256) void k_sh_rest_project(ViewK v, GaussK g, int mode, const float* __restrict__ in,
                                                          int64_t in_stride, float* __restrict__ out,
                                                          int64_t out_stride) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.P) return;
-  const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
-  const float dx = x - v.campos[0], dy = y - v.campos[1], dz = z - v.campos[2];
-  const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
-  float B[16];
-  sh_basis(v.D, dx / len, dy / len, dz / len, B);
-  const int nc = (v.D + 1) * (v.D + 1);
-  const float nb = sh_rest_norm(B, nc);
-  const float inv = nb > 0.f ? 1.f / nb : 0.f;
-  if (mode == 0) {
-    for (int k = 1; k < g.M; ++k)
+  // the block's [256, M-1, 3] rows go through LDS so the full-layout side is read / written coalesced
+  extern __shared__ __attribute__((aligned(16))) float s_rows[];
+  const int R = 3 * (g.M - 1);
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+  const int64_t i = i0 + threadIdx.x;
+  if (mode == 1) {  // gather the rows to project
+    for (int64_t e = threadIdx.x; e < nv * R; e += blockDim.x) {
+      const int64_t ii = e / R, r = e - ii * R;
+      s_rows[e] = in[(i0 + ii) * in_stride + r];
+    }
+    __syncthreads();
+  }
+  if (i < g.P) {
+    const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
+    const float dx = x - v.campos[0], dy = y - v.campos[1], dz = z - v.campos[2];
+    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+    float B[16];
+    sh_basis(v.D, dx / len, dy / len, dz / len, B);
+    const int nc = (v.D + 1) * (v.D + 1);
+    const float nb = sh_rest_norm(B, nc);
+    const float inv = nb > 0.f ? 1.f / nb : 0.f;
+    float* row = s_rows + (int64_t)threadIdx.x * R;
+    if (mode == 0) {
+      for (int k = 1; k < g.M; ++k)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) out[i * out_stride + 3 * (k - 1) + c] = k < nc ? (B[k] * inv) * in[i * in_stride + c] : 0.f;
-  } else {
-    float acc[3] = {0.f, 0.f, 0.f};
-    for (int k = 1; k < g.M && k < nc; ++k)
+        for (int c = 0; c < 3; ++c) row[3 * (k - 1) + c] = k < nc ? (B[k] * inv) * in[i * in_stride + c] : 0.f;
+    } else {
+      float acc[3] = {0.f, 0.f, 0.f};
+      for (int k = 1; k < g.M && k < nc; ++k)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) acc[c] += (B[k] * inv) * in[i * in_stride + 3 * (k - 1) + c];
+        for (int c = 0; c < 3; ++c) acc[c] += (B[k] * inv) * row[3 * (k - 1) + c];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[i * out_stride + c] = acc[c];
+      for (int c = 0; c < 3; ++c) out[i * out_stride + c] = acc[c];
+    }
+  }
+  if (mode == 0) {  // scatter the expanded rows
+    __syncthreads();
+    for (int64_t e = threadIdx.x; e < nv * R; e += blockDim.x) {
+      const int64_t ii = e / R, r = e - ii * R;
+      out[(i0 + ii) * out_stride + r] = s_rows[e];
+    }
   }
 }
 
@@ -141,7 +162,8 @@ __global__ __launch_bounds__(256) void k_sh_rest_project(ViewK v, GaussK g, int 
 int launch_sh_rest_project(const ViewK& v, const GaussK& g, int mode, const float* in, int64_t in_stride, float* out,
                            int64_t out_stride, hipStream_t s) {
   if (g.P == 0 || g.M < 2) return GSLM_OK;
-  hipLaunchKernelGGL(k_sh_rest_project, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, v, g, mode, in,
+  const size_t lds = (size_t)256 * 3 * (g.M - 1) * sizeof(float);
+  hipLaunchKernelGGL(k_sh_rest_project, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, v, g, mode, in,
                      in_stride, out, out_stride);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
