@@ -75,39 +75,45 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
   if (tid == 0) totals[d] = carry;
 }
 
+// Scatter of one pass: the block ranks its 4096 keys by digit (stable: round, then wave, then lane order),
+// reorders them through LDS into digit-sorted order, and writes each digit's run to its global offset
+// from consecutive threads -- coalesced segments instead of one scattered 4-byte store per key.
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, const uint32_t* __restrict__ hist, int nblocks,
     const uint32_t* __restrict__ totals) {
-  __shared__ uint32_t s_base[RADIX];
+  __shared__ uint32_t s_keys[SORT_TILE], s_vals[SORT_TILE];
+  __shared__ uint32_t s_run[RADIX];    // running per-digit count in this block, then the digit's local start
+  __shared__ uint32_t s_gbase[RADIX];  // global offset of this block's run of each digit
   __shared__ uint32_t s_wc[4][RADIX];
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+  const int nvalid = (int)min<int64_t>(SORT_TILE, n - base);
 
   // issue all loads first (16 keys + 16 values per thread in flight)
-  uint32_t key[SORT_ITEMS], val[SORT_ITEMS];
+  uint32_t key[SORT_ITEMS], val[SORT_ITEMS], lidx[SORT_ITEMS];
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
     const int64_t i = base + r * SORT_THREADS + tid;
     key[r] = i < n ? kin[i] : 0u;
     val[r] = i < n ? vin[i] : 0u;
   }
-
-  // digit base for this block = exclusive prefix of digit totals + this block's offset
   {
+    // digit base for this block = exclusive prefix of digit totals + this block's offset
     const uint32_t t = totals[tid];
     uint32_t tot;
     const uint32_t inc = block_incl_scan256(t, s_w, &tot);
-    s_base[tid] = inc - t + hist[(int64_t)tid * nblocks + blockIdx.x];
+    s_gbase[tid] = inc - t + hist[(int64_t)tid * nblocks + blockIdx.x];
+    s_run[tid] = 0u;
   }
   __syncthreads();
 
+  // 1. local rank of every key within its digit (elements of one round: wave order, then lane order)
   const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
-    const int64_t i = base + r * SORT_THREADS + tid;
-    const bool valid = i < n;
+    const bool valid = r * SORT_THREADS + tid < nvalid;
     const uint32_t d = (key[r] >> shift) & (RADIX - 1);
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_wc[w][lane + 64 * k] = 0u;
@@ -123,20 +129,42 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     __syncthreads();
     {
       const uint32_t c0 = s_wc[0][tid], c1 = s_wc[1][tid], c2 = s_wc[2][tid], c3 = s_wc[3][tid];
-      const uint32_t b0 = s_base[tid];
+      const uint32_t b0 = s_run[tid];
       s_wc[0][tid] = b0;
       s_wc[1][tid] = b0 + c0;
       s_wc[2][tid] = b0 + c0 + c1;
       s_wc[3][tid] = b0 + c0 + c1 + c2;
-      s_base[tid] = b0 + c0 + c1 + c2 + c3;
+      s_run[tid] = b0 + c0 + c1 + c2 + c3;
     }
     __syncthreads();
-    if (valid) {
-      const uint32_t pos = s_wc[w][d] + rank;
-      kout[pos] = key[r];
-      vout[pos] = val[r];
-    }
+    lidx[r] = s_wc[w][d] + rank;
     __syncthreads();
+  }
+  // 2. digit-sorted order in LDS: local start of each digit = exclusive prefix of the block's counts
+  {
+    const uint32_t c = s_run[tid];
+    uint32_t tot;
+    const uint32_t inc = block_incl_scan256(c, s_w, &tot);
+    s_run[tid] = inc - c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    if (r * SORT_THREADS + tid < nvalid) {
+      const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+      const uint32_t lp = s_run[d] + lidx[r];
+      s_keys[lp] = key[r];
+      s_vals[lp] = val[r];
+    }
+  }
+  __syncthreads();
+  // 3. each run to its global offset, consecutive threads on consecutive elements
+  for (int e = tid; e < nvalid; e += SORT_THREADS) {
+    const uint32_t k = s_keys[e];
+    const uint32_t d = (k >> shift) & (RADIX - 1);
+    const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_run[d]);
+    kout[pos] = k;
+    vout[pos] = s_vals[e];
   }
 }
 
