@@ -56,27 +56,58 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   if (radii_out) radii_out[i] = o.radius;
 }
 
+// One block per 256 consecutive Gaussians of the depth order: their (tile, id) pairs are one contiguous
+// output range, written by the whole block in element order (coalesced, and a large Gaussian's tiles are
+// spread over the block instead of one thread's loop).  Element e belongs to the last Gaussian whose
+// local offset is <= e (binary search in LDS); inside a Gaussian the rect is walked row-major.
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                     const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint2* __restrict__ rect, const float4* __restrict__ rec,
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= P) return;
-  const uint32_t g = sorted_idx[s];
-  const uint32_t n = tiles[g];
-  if (n == 0) return;
-  uint32_t off = offsets[s];
-  const uint2 rc = rect[g];
-  const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF, y1 = rc.y >> 16;
-  const float4 r0 = rec[3 * (int64_t)g + 0];
-  const QuadCull qc = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, rec[3 * (int64_t)g + 1].x, rec[3 * (int64_t)g + 2].w);
-  for (int ty = y0; ty < y1; ++ty)
-    for (int tx = x0; tx < x1; ++tx) {
-      keys[off] = (uint32_t)(ty * gx + tx);
-      vals[off] = g | (quad_mask(qc, tx, ty) << ID_BITS);
-      ++off;
+  __shared__ QuadCull s_q[256];
+  __shared__ uint32_t s_off[257];
+  __shared__ uint32_t s_g[256];
+  __shared__ uint32_t s_rc[256][3];  // x0, y0, width
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
+  const int64_t slast = min(s0 + 255, P - 1);
+  const uint32_t base = offsets[s0];
+  uint32_t n = 0;
+  if (s < P) {
+    const uint32_t g = sorted_idx[s];
+    n = tiles[g];
+    s_off[tid] = offsets[s] - base;
+    if (n) {
+      const uint2 rc = rect[g];
+      const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
+      s_rc[tid][0] = (uint32_t)x0;
+      s_rc[tid][1] = (uint32_t)y0;
+      s_rc[tid][2] = (uint32_t)(x1 - x0);
+      s_g[tid] = g;
+      const float4 r0 = rec[3 * (int64_t)g + 0];
+      s_q[tid] = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, rec[3 * (int64_t)g + 1].x, rec[3 * (int64_t)g + 2].w);
     }
+  } else {
+    s_off[tid] = 0xFFFFFFFFu;  // past the block's last Gaussian: never an owner
+  }
+  if (s == slast) s_off[256] = offsets[s] - base + n;
+  __syncthreads();
+  const uint32_t total = s_off[256];
+  for (uint32_t e = tid; e < total; e += 256) {
+    int lo = 0, hi = 255;  // last t with s_off[t] <= e (s_off[0] = 0)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t li = e - s_off[lo];
+    const uint32_t w = s_rc[lo][2];
+    const uint32_t dy = li / w;
+    const int tx = (int)(s_rc[lo][0] + (li - dy * w)), ty = (int)(s_rc[lo][1] + dy);
+    keys[base + e] = (uint32_t)(ty * gx + tx);
+    vals[base + e] = s_g[lo] | (quad_mask(s_q[lo], tx, ty) << ID_BITS);
+  }
 }
 
 // Launch order of the tile passes: tiles by descending list length (a longest-first schedule, so the
