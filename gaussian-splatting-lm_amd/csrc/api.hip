@@ -21,11 +21,6 @@ struct Carver {
   }
 };
 
-__global__ void k_iota(uint32_t* out, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (uint32_t)i;
-}
-
 }  // namespace
 
 size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
@@ -146,14 +141,14 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
     GSLM_HIP_CHECK(hipMemsetAsync(gb.counters, 0, 4, s));
     return GSLM_OK;
   }
-  hipLaunchKernelGGL(k_iota, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, gb.vals_init, P);
-  GSLM_LAUNCH_CHECK();
+  // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass)
   bool alt = false;
-  st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s);
+  st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true);
   if (st) return st;
   if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
-  if ((st = exclusive_scan_u32(gb.tiles, nullptr, gb.goff, P, gb.scan_tmp, gb.counters + 1, s))) return st;
-  return exclusive_scan_u32(gb.tiles, gb.sorted_idx, gb.offsets, P, gb.scan_tmp, gb.counters, s);
+  // tile-count scans in index order (gradient-row offsets goff) and in depth order (duplicate offsets)
+  return exclusive_scan_u32_dual(gb.tiles, gb.sorted_idx, gb.goff, gb.offsets, P, gb.scan_tmp, gb.counters + 1,
+                                 gb.counters, s);
 }
 
 }  // namespace gslm

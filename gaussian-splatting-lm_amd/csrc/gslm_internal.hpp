@@ -43,16 +43,19 @@ inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_b
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
 // ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
-                     uint32_t* hist, bool* result_in_alt, hipStream_t s);
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false);
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 inline int64_t scan_blocks(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
-inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n) * 4 + 64); }
+inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n) * 8 + 64); }  // dual scans: 2 nb
 // out[i] = sum_{j<i} in[idx ? idx[j] : j];  *total (device) = full sum.
 int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
                        uint32_t* total, hipStream_t s);
+// out_a[i] = sum_{j<i} in[j], out_b[i] = sum_{j<i} in[idx[j]] in one pass (tmp: scan_tmp_bytes(n)).
+int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* out_a, uint32_t* out_b, int64_t n,
+                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s);
 
 }  // namespace gslm

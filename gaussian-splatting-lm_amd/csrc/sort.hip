@@ -97,7 +97,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   for (int r = 0; r < SORT_ITEMS; ++r) {
     const int64_t i = base + r * SORT_THREADS + tid;
     key[r] = i < n ? kin[i] : 0u;
-    val[r] = i < n ? vin[i] : 0u;
+    val[r] = i < n ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == NULL: the values are the indices
   }
   {
     // digit base for this block = exclusive prefix of digit totals + this block's offset
@@ -228,21 +228,116 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __r
   }
 }
 
+// Two exclusive scans of the same counts in one pass: in index order (out_a) and gathered through idx
+// (out_b).  block_sums holds 2 nb partials: [0, nb) for a, [nb, 2 nb) for b.
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan2_reduce(const uint32_t* __restrict__ in,
+                                                               const uint32_t* __restrict__ idx, int64_t n,
+                                                               uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  uint32_t acc_a = 0, acc_b = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) {
+      acc_a += in[i];
+      acc_b += in[idx[i]];
+    }
+  }
+  uint32_t tot_a, tot_b;
+  block_incl_scan256(acc_a, s_w, &tot_a);
+  block_incl_scan256(acc_b, s_w, &tot_b);
+  if (tid == 0) {
+    block_sums[blockIdx.x] = tot_a;
+    block_sums[gridDim.x + blockIdx.x] = tot_b;
+  }
+}
+
+// blockIdx.x = 0 scans the a partials, 1 the b partials
+__global__ __launch_bounds__(256) void k_scan2_top(uint32_t* __restrict__ block_sums, int nb,
+                                                   uint32_t* __restrict__ total_a, uint32_t* __restrict__ total_b) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  uint32_t* bs = block_sums + (int64_t)blockIdx.x * nb;
+  uint32_t carry = 0;
+  for (int base = 0; base < nb; base += 256) {
+    const int i = base + tid;
+    const uint32_t x = i < nb ? bs[i] : 0u;
+    uint32_t tot;
+    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
+    if (i < nb) bs[i] = carry + inc - x;
+    carry += tot;
+  }
+  if (tid == 0) *(blockIdx.x == 0 ? total_a : total_b) = carry;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __restrict__ in,
+                                                              const uint32_t* __restrict__ idx, int64_t n,
+                                                              const uint32_t* __restrict__ block_sums,
+                                                              uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  uint32_t va[SCAN_ITEMS], vb[SCAN_ITEMS];
+  uint32_t acc_a = 0, acc_b = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    va[k] = i < n ? in[i] : 0u;
+    vb[k] = i < n ? in[idx[i]] : 0u;
+    acc_a += va[k];
+    acc_b += vb[k];
+  }
+  uint32_t tot;
+  const uint32_t inc_a = block_incl_scan256(acc_a, s_w, &tot);
+  const uint32_t inc_b = block_incl_scan256(acc_b, s_w, &tot);
+  uint32_t ra = block_sums[blockIdx.x] + inc_a - acc_a;
+  uint32_t rb = block_sums[gridDim.x + blockIdx.x] + inc_b - acc_b;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) {
+      out_a[i] = ra;
+      out_b[i] = rb;
+    }
+    ra += va[k];
+    rb += vb[k];
+  }
+}
+
 }  // namespace
 
+int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* out_a, uint32_t* out_b, int64_t n,
+                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s) {
+  if (n <= 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(total_a, 0, 4, s));
+    GSLM_HIP_CHECK(hipMemsetAsync(total_b, 0, 4, s));
+    return GSLM_OK;
+  }
+  const int nb = (int)scan_blocks(n);
+  hipLaunchKernelGGL(k_scan2_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
+  hipLaunchKernelGGL(k_scan2_top, dim3(2), dim3(256), 0, s, tmp, nb, total_a, total_b);
+  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out_a, out_b);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
-                     uint32_t* hist, bool* result_in_alt, hipStream_t s) {
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const int nb = (int)sort_blocks(n);
   uint32_t* totals = hist + (size_t)RADIX * nb;
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+  bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
   bool alt = false;
   for (int shift = 0; shift < end_bit; shift += 8) {
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vi, ko, vo, n, shift, hist,
-                       nb, totals);
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki,
+                       (first && iota_values) ? (const uint32_t*)nullptr : vi, ko, vo, n, shift, hist, nb, totals);
+    first = false;
     GSLM_LAUNCH_CHECK();
     std::swap(ki, ko);
     std::swap(vi, vo);
