@@ -316,6 +316,49 @@ int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussia
                     (hipStream_t)stream);
 }
 
+// The fused CG direction update of gslm_matvec_opts (xpby_s .. xpby_x_offset) as a kernel argument; R is
+// the SH-rest width of v and s (3(M-1), or 3 projected).
+static int build_xpby(const gslm_matvec_opts* opts, const gslm_grads* vin, int R, bool mask_xyz, XpbyK* out) {
+  const gslm_grads* sv = opts->xpby_s;
+  if (!opts->beta_num || !opts->beta_den) {
+    set_error("matvec: xpby needs the TANGENT stage and beta_num / beta_den");
+    return GSLM_ERR_INVALID;
+  }
+  if (vin->sh_dc_stride != 3 || sv->sh_dc_stride != 3 || (R > 0 && (vin->sh_rest_stride != R || sv->sh_rest_stride != R))) {
+    set_error("matvec: xpby needs contiguous SH groups (dc stride 3, rest stride 3(M-1), or 3 projected)");
+    return GSLM_ERR_INVALID;
+  }
+  XpbyK xp{};
+  float* pp[6] = {vin->means3D, vin->sh_dc, vin->sh_rest, vin->scales, vin->rotations, vin->opacities};
+  const float* ss[6] = {sv->means3D, sv->sh_dc, sv->sh_rest, sv->scales, sv->rotations, sv->opacities};
+  const int ww[6] = {3, 3, R, 3, 4, 1};
+  for (int k = 0; k < 6; ++k) {
+    if ((pp[k] == nullptr) != (ss[k] == nullptr) || (ww[k] == 0 && pp[k])) {
+      set_error("matvec: xpby groups of v and s must match");
+      return GSLM_ERR_INVALID;
+    }
+    // with mask_xyz the xyz group is left untouched: it is zero in every LM iterate (s and p alike)
+    xp.p[k] = (ww[k] && !(k == 0 && mask_xyz)) ? pp[k] : nullptr;
+    xp.s[k] = ss[k];
+    xp.w[k] = ww[k];
+  }
+  xp.num = opts->beta_num;
+  xp.den = opts->beta_den;
+  xp.tail_p = opts->xpby_tail_n > 0 ? opts->xpby_tail_v : nullptr;
+  xp.tail_s = opts->xpby_tail_s;
+  xp.tail_n = opts->xpby_tail_n;
+  if (xp.tail_p && !xp.tail_s) { set_error("matvec: xpby tail without s"); return GSLM_ERR_INVALID; }
+  xp.anum = opts->alpha_num;
+  xp.aden = opts->alpha_den;
+  xp.xoff = opts->xpby_x_offset / (int64_t)sizeof(float);
+  if (xp.anum && (!xp.aden || opts->xpby_x_offset % (int64_t)sizeof(float) != 0)) {
+    set_error("matvec: deferred x update needs alpha_den and a float-aligned xpby_x_offset");
+    return GSLM_ERR_INVALID;
+  }
+  *out = xp;
+  return GSLM_OK;
+}
+
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                         int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
@@ -349,42 +392,18 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   XpbyK xp{};
   const bool fused_xpby = opts && opts->xpby_s;
   if (fused_xpby) {
-    const gslm_grads* sv = opts->xpby_s;
-    if (!(stages & GSLM_STAGE_TANGENT) || !opts->beta_num || !opts->beta_den) {
+    if (!(stages & GSLM_STAGE_TANGENT)) {
       set_error("matvec: xpby needs the TANGENT stage and beta_num / beta_den");
       return GSLM_ERR_INVALID;
     }
-    const int R = proj ? 3 : 3 * (b.g.M - 1);
-    if (vin->sh_dc_stride != 3 || sv->sh_dc_stride != 3 || (b.g.M > 1 && (vin->sh_rest_stride != R || sv->sh_rest_stride != R))) {
-      set_error("matvec: xpby needs contiguous SH groups (dc stride 3, rest stride 3(M-1), or 3 projected)");
+    if ((st = build_xpby(opts, vin, proj ? 3 : 3 * (b.g.M - 1), mask_xyz != 0, &xp))) return st;
+  }
+  if (opts && opts->trec_in) {
+    if (stages & GSLM_STAGE_TANGENT) {
+      set_error("matvec: trec_in replaces the TANGENT stage");
       return GSLM_ERR_INVALID;
     }
-    float* pp[6] = {vin->means3D, vin->sh_dc, vin->sh_rest, vin->scales, vin->rotations, vin->opacities};
-    const float* ss[6] = {sv->means3D, sv->sh_dc, sv->sh_rest, sv->scales, sv->rotations, sv->opacities};
-    const int ww[6] = {3, 3, R, 3, 4, 1};
-    for (int k = 0; k < 6; ++k) {
-      if ((pp[k] == nullptr) != (ss[k] == nullptr) || (ww[k] == 0 && pp[k])) {
-        set_error("matvec: xpby groups of v and s must match");
-        return GSLM_ERR_INVALID;
-      }
-      // with mask_xyz the xyz group is left untouched: it is zero in every LM iterate (s and p alike)
-      xp.p[k] = (ww[k] && !(k == 0 && mask_xyz)) ? pp[k] : nullptr;
-      xp.s[k] = ss[k];
-      xp.w[k] = ww[k];
-    }
-    xp.num = opts->beta_num;
-    xp.den = opts->beta_den;
-    xp.tail_p = opts->xpby_tail_n > 0 ? opts->xpby_tail_v : nullptr;
-    xp.tail_s = opts->xpby_tail_s;
-    xp.tail_n = opts->xpby_tail_n;
-    if (xp.tail_p && !xp.tail_s) { set_error("matvec: xpby tail without s"); return GSLM_ERR_INVALID; }
-    xp.anum = opts->alpha_num;
-    xp.aden = opts->alpha_den;
-    xp.xoff = opts->xpby_x_offset / (int64_t)sizeof(float);
-    if (xp.anum && (!xp.aden || opts->xpby_x_offset % (int64_t)sizeof(float) != 0)) {
-      set_error("matvec: deferred x update needs alpha_den and a float-aligned xpby_x_offset");
-      return GSLM_ERR_INVALID;
-    }
+    b.sb.trec = reinterpret_cast<float4*>(const_cast<float*>(opts->trec_in));
   }
   const float* seed = opts ? opts->pixel_seed : nullptr;
   if (seed && (!mask_xyz || fused_xpby || (stages & (GSLM_STAGE_TANGENT | GSLM_STAGE_SCREEN)))) {
@@ -472,11 +491,54 @@ int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussi
     return GSLM_ERR_CAPACITY;
   }
   double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
-  if ((st = launch_gather_screen(vk, nviews, g, screen, make_gradk(y), make_gradk(vin), damp7,
+  const int64_t sstride = (opts && opts->screen_stride) ? opts->screen_stride : g.P;
+  if (sstride < g.P) { set_error("gather_screen: screen_stride below P"); return GSLM_ERR_INVALID; }
+  if ((st = launch_gather_screen(vk, nviews, g, screen, sstride, make_gradk(y), make_gradk(vin), damp7,
                                  (stages & GSLM_STAGE_OVERWRITE) != 0, part, (hipStream_t)stream)))
     return st;
   if (dot_out) return gslm_dot_finalize(part, (int32_t)((g.P + 255) / 256), dot_out, stream);
   return GSLM_OK;
+}
+
+int gslm_view_flags(const void* geom, int64_t P, uint32_t* out, void* stream) {
+  if (P < 0 || (P > 0 && (!geom || !out))) { set_error("view_flags: NULL geom / out"); return GSLM_ERR_INVALID; }
+  GeomBufs gb;
+  geom_layout(P, const_cast<void*>(geom), &gb);
+  return launch_view_flags(P, gb, out, (hipStream_t)stream);
+}
+
+int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, const gslm_grads* vin,
+                       int32_t mask_xyz, const uint32_t* vflags, int64_t flags_stride, float* trec_out,
+                       int64_t trec_stride, const gslm_matvec_opts* opts, void* stream) {
+  if (!views || nviews < 1 || nviews > MAX_SCREEN_VIEWS || !gi || !vin) {
+    set_error("tangent_views: NULL argument or nviews outside 1..16");
+    return GSLM_ERR_INVALID;
+  }
+  ViewK vk[MAX_SCREEN_VIEWS];
+  GaussK g;
+  int st;
+  for (int b = 0; b < nviews; ++b)
+    if ((st = make_view(&views[b], gi->max_coeffs, &vk[b]))) return st;
+  if ((st = make_gauss(gi, &vk[0], &g, false))) return st;
+  if (!g.raw || g.cov3D || g.colors) {
+    set_error("tangent_views: gaussians must be the raw GaussianModel leaves (raw = 1)");
+    return GSLM_ERR_INVALID;
+  }
+  if (g.P > 0 && (!vflags || !trec_out || flags_stride < g.P || trec_stride < g.P)) {
+    set_error("tangent_views: NULL vflags / trec_out or a stride below P");
+    return GSLM_ERR_INVALID;
+  }
+  GaussK t = tangent_from_grads(vin, g, mask_xyz != 0);
+  const int R = 3 * (g.M - 1);
+  if (t.rest && t.rest_stride != R) {
+    set_error("tangent_views: the SH-rest tangent needs stride 3(M-1)");
+    return GSLM_ERR_INVALID;
+  }
+  XpbyK xp{};
+  const bool fused = opts && opts->xpby_s;
+  if (fused && (st = build_xpby(opts, vin, R, mask_xyz != 0, &xp))) return st;
+  return launch_tangent_views(vk, nviews, g, t, vflags, flags_stride, trec_out, trec_stride, fused ? &xp : nullptr,
+                              (hipStream_t)stream);
 }
 
 int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,

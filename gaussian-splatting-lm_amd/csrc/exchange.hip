@@ -15,12 +15,6 @@
 
 namespace gslm {
 
-constexpr int MAX_SCREEN_VIEWS = 16;
-struct ViewsK {
-  ViewK v[MAX_SCREEN_VIEWS];
-  int n;
-};
-
 __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* __restrict__ rec,
                                                         const uint32_t* __restrict__ tiles,
                                                         const uint32_t* __restrict__ goff,
@@ -41,7 +35,7 @@ __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* 
 }
 
 __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, const float4* __restrict__ screen,
-                                                        FlatK o) {
+                                                        int64_t sstride, FlatK o) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
   __shared__ double s_dot[4];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,8 +50,8 @@ __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, cons
   if (i < g.P) {
 #pragma unroll 1
     for (int b = 0; b < vs.n; ++b) {
-      const float4 a = screen[2 * ((int64_t)b * g.P + i) + 0];
-      const float4 c = screen[2 * ((int64_t)b * g.P + i) + 1];
+      const float4 a = screen[2 * ((int64_t)b * sstride + i) + 0];
+      const float4 c = screen[2 * ((int64_t)b * sstride + i) + 1];
       const uint32_t flags = __float_as_uint(c.w);
       if (!(flags >> 31)) continue;
       const float G2[NV] = {0.f, 0.f, a.x, a.y, a.z, a.w, c.x, c.y, c.z, 0.f};
@@ -87,8 +81,9 @@ int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs&
   return GSLM_OK;
 }
 
-int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, const GradK& y,
-                         const GradK& vin, const double* damp7, bool overwrite, double* dot_part, hipStream_t s) {
+int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, int64_t sstride,
+                         const GradK& y, const GradK& vin, const double* damp7, bool overwrite, double* dot_part,
+                         hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   FlatK o;
   const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o);
@@ -102,7 +97,23 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
   vs.n = nviews;
   const size_t lds = sh_stage_floats<false>(g.M) * sizeof(float) + 16;
   hipLaunchKernelGGL(k_gather_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, vs, g,
-                     reinterpret_cast<const float4*>(screen), o);
+                     reinterpret_cast<const float4*>(screen), sstride, o);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+// Visibility / SH-clamp word of every Gaussian of a preprocessed view (the SCREEN rows' flags), for
+// the Gaussian-sharded exchange's once-per-geometry all-to-all.
+__global__ __launch_bounds__(256) void k_view_flags(int64_t P, const float4* __restrict__ rec,
+                                                     const uint32_t* __restrict__ tiles, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  out[i] = tiles[i] ? (0x80000000u | (__float_as_uint(rec[3 * i + 2].z) & 7u)) : 0u;
+}
+
+int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s) {
+  if (P == 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, gb.rec, gb.tiles, out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

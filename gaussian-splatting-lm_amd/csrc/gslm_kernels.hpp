@@ -379,8 +379,17 @@ struct XpbyK {
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                        const ScratchBufs& sb, const XpbyK* xp, hipStream_t s);
 int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s);
-int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, const GradK& y,
-                         const GradK& vin, const double* damp7, bool overwrite, double* dot_part, hipStream_t s);
+constexpr int MAX_SCREEN_VIEWS = 16;
+struct ViewsK {
+  ViewK v[MAX_SCREEN_VIEWS];
+  int n;
+};
+int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, int64_t sstride,
+                         const GradK& y, const GradK& vin, const double* damp7, bool overwrite, double* dot_part,
+                         hipStream_t s);
+int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s);
+int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s);
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);

@@ -124,4 +124,72 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
   return GSLM_OK;
 }
 
+// Gaussian-sharded exchange: the tangent render records of a Gaussian range for several views (the
+// TANGENT stage of k_preprocess_jvp, looped over views), after the optional fused direction update.
+// The block's SH-rest tangent slice is staged in LDS once and read by every view's chain.
+template <bool XPBY>
+__global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, GaussK t, const uint32_t* __restrict__ vflags,
+                                                        int64_t fstride, float4* __restrict__ out, int64_t ostride,
+                                                        XpbyK xp) {
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + threadIdx.x;
+  if (XPBY) {
+    block_xpby(xp, g.P, s_rest);
+  } else if (t.rest) {
+    const int64_t len = min((int64_t)blockDim.x, g.P - i0) * t.rest_stride;
+    const float* src = t.rest + i0 * t.rest_stride;
+    for (int64_t e = threadIdx.x; e < len; e += blockDim.x) s_rest[e] = src[e];
+  }
+  __syncthreads();
+  if (t.rest) {
+    t.rest = s_rest;
+    t.rest_base = i0;
+  }
+  if (i >= g.P) return;
+#pragma unroll 1
+  for (int b = 0; b < vs.n; ++b) {
+    const uint32_t f = vflags[(int64_t)b * fstride + i];
+    if (!(f >> 31)) continue;
+    float T2[10];
+    chain_jvp<true>(vs.v[b], g, t, nullptr, i, f & 7u, T2);
+    float4* o = out + 3 * ((int64_t)b * ostride + i);
+    o[0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
+    o[1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
+    o[2] = make_float4(T2[8], T2[9], 0.f, 0.f);
+  }
+}
+
+int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s) {
+  if (nviews < 1 || nviews > MAX_SCREEN_VIEWS) {
+    set_error("tangent_views: 1..16 views per call");
+    return GSLM_ERR_INVALID;
+  }
+  if (g.P == 0) {
+    if (xp && xp->tail_p) {
+      set_error("tangent_views: fused xpby with P = 0");
+      return GSLM_ERR_INVALID;
+    }
+    return GSLM_OK;
+  }
+  if (xp && t.rest && (t.rest != xp->p[2] || t.rest_stride != xp->w[2])) {
+    set_error("internal: fused xpby expects the tangent's SH-rest group to be p's");
+    return GSLM_ERR_INVALID;
+  }
+  ViewsK vs;
+  for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
+  vs.n = nviews;
+  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const size_t lds = t.rest ? (size_t)256 * t.rest_stride * sizeof(float) : 0;
+  XpbyK none{};
+  float4* o = reinterpret_cast<float4*>(out);
+  if (xp)
+    hipLaunchKernelGGL(k_tangent_views<true>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, *xp);
+  else
+    hipLaunchKernelGGL(k_tangent_views<false>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, none);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 }  // namespace gslm

@@ -59,6 +59,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("xpby_tail_v", ctypes.c_void_p), ("xpby_tail_s", ctypes.c_void_p), ("xpby_tail_n", ctypes.c_int64),
         ("screen_out", ctypes.c_void_p), ("pixel_seed", ctypes.c_void_p), ("jv_out", ctypes.c_void_p),
         ("alpha_num", ctypes.c_void_p), ("alpha_den", ctypes.c_void_p), ("xpby_x_offset", ctypes.c_int64),
+        ("trec_in", ctypes.c_void_p), ("screen_stride", ctypes.c_int64),
     ]
 
 
@@ -114,6 +115,10 @@ EXPORTS = {
     "gslm_gather_screen": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
                                           ctypes.c_void_p, ctypes.POINTER(GslmGrads), ctypes.POINTER(GslmGrads),
                                           ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_view_flags": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_tangent_views": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
+                                          ctypes.POINTER(GslmGrads), ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_cg_update": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]),
@@ -169,7 +174,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 2  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 3  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):

@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 2
+#define GSLM_ABI_VERSION 3
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -208,6 +208,12 @@ typedef struct gslm_matvec_opts {
   const double* alpha_num;
   const double* alpha_den;
   int64_t xpby_x_offset;
+  /* Gaussian-sharded exchange (gslm_tangent_views below): when set, RENDER reads this view's tangent render
+   * records ([>= P][12] floats, gslm_tangent_views' output once exchanged) instead of the TANGENT stage's
+   * (TANGENT must be off). */
+  const float* trec_in;
+  /* gslm_gather_screen only: Gaussians between consecutive views' blocks of screen (0 means P). */
+  int64_t screen_stride;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
@@ -233,6 +239,28 @@ int gslm_sh_rest_project(const gslm_view* view, const gslm_gaussians* g, int32_t
  * call (accumulate further calls).  Replaces the reduction of solver_functions.py:110-121. */
 int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const float* screen,
                        const gslm_grads* v, const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
+
+/* ---- Gaussian-sharded exchange (multi-GPU LM product; gslm.parallel, exchange "gaussian") ----
+ * Rank r owns Gaussians [r S, (r + 1) S) of every CG vector and the vector algebra on them.  Per product:
+ *   gslm_tangent_views   this shard's tangent render records for EVERY view b (chain_jvp, the TANGENT stage
+ *                        of gslm_matvec_view_ex for a Gaussian range) -> all-to-all -> each rank holds its
+ *                        own view's [P][12] table for opts->trec_in;
+ *   RENDER | SCREEN      with opts->trec_in -> [P][8] screen sums -> all-to-all -> each rank holds
+ *                        screen[b][S][8] of its shard for every view;
+ *   gslm_gather_screen   over the shard (g = the shard's slice of the leaves, opts->screen_stride = S).
+ * A rank receives (48 + 32) (n - 1) / n bytes per Gaussian per view it renders instead of the screen
+ * all-gather's 32 (n - 1), and runs 1/n of the chains and vector algebra.
+ * gslm_view_flags: out[i] = 0 if Gaussian i touches no tile of the preprocessed view, else
+ * 0x80000000 | its 3 SH-clamp bits (the flags word of the SCREEN rows); exchanged once per geometry. */
+int gslm_view_flags(const void* geom, int64_t P, uint32_t* out, void* stream);
+/* trec_out[(b trec_stride + i) * 12 ..] = tangent render record of shard Gaussian i in view b where
+ * vflags[b flags_stride + i] is visible (other records untouched), b < nviews (<= 16).  g / v: the shard's
+ * leaves and direction (P = shard size, SH-rest stride 3(M-1)); opts (or NULL): only the fused direction
+ * update (xpby_s, beta_*, alpha_*, xpby_x_offset, xpby_tail_*) of gslm_matvec_view_ex, applied once before
+ * the views' tangents. */
+int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const gslm_grads* v,
+                       int32_t mask_xyz, const uint32_t* vflags, int64_t flags_stride, float* trec_out,
+                       int64_t trec_stride, const gslm_matvec_opts* opts, void* stream);
 
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */
