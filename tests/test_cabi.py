@@ -51,6 +51,16 @@ def test_invalid_arguments_return_error_codes():
     g = _lib.make_gaussians(10)  # P > 0 but no tensors
     assert lib.gslm_preprocess(ctypes.byref(view), ctypes.byref(g), None, 0, None, None) == _lib.GSLM_ERR_INVALID
     assert lib.gslm_damp_add(10, None, None, None, 9, None, None) == _lib.GSLM_ERR_INVALID
+    # Gaussian-sharded exchange entry points (ABI v3)
+    assert lib.gslm_view_flags(None, 10, None, None) == _lib.GSLM_ERR_INVALID
+    assert b"view_flags" in lib.gslm_last_error()
+    views = (_lib.GslmView * 17)(*([view] * 17))
+    g = _lib.make_gaussians(0)
+    v = _lib.GslmGrads()
+    for n in (0, 17):
+        assert lib.gslm_tangent_views(views, n, ctypes.byref(g), ctypes.byref(v), 1, None, 0, None, 0, None,
+                                      None) == _lib.GSLM_ERR_INVALID
+        assert b"nviews" in lib.gslm_last_error()
 
 
 def test_dropin_modules_import_with_reference_names():
