@@ -51,9 +51,33 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args):
+    """`python bench.py --gpus N` without a launcher: start N ranks as child processes (one per GPU, RCCL) with the
+    torchrun environment, before this process touches the GPU, and exit with the worst child's code.  Rank 0's
+    stdout (the JSON line) passes through."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_size}: launch one rank per GPU "
+                         f"(torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}, or bench.py --gpus N alone)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # GSLM_BENCH_DIST=gloo rehearses the multi-rank path with several ranks on one GPU (host-staged
@@ -224,6 +248,20 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # list entries any pixel of their tile can blend (sum over tiles of max n_contrib): the tile passes read only
+    # these (positions past a tile's last blended entry are skipped), N_dup counts every binned pair
+    ts = tile_stats(vr, args.P)
+    alg_visited = 168 * ts["visited_entries"] + 20 * HW
+    # forward raster against SURVEY 8(d)'s B_fwd per view (params 4F P, preprocess state 48 P, 88 per list entry:
+    # key/value write 12 + one sort read/write 24 + range scan 8 + render gather 44, 24 per pixel)
+    F = 11 + 3 * (args.sh + 1) ** 2
+    b_fwd = 4 * F * args.P + 48 * args.P + 88 * N0 + 24 * HW
+    fwd_s = t_fwd / fsteps / max(len(prob.views), 1)
+    raster_roofline = {"bound": "hbm", "achieved": b_fwd / fwd_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": b_fwd / fwd_s / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_view": b_fwd,
+                       "model": "SURVEY 8(d) B_fwd = 4F P + 48 P + 88 N_dup + 24 HW, over the full forward "
+                                "(preprocess, depth sort, binning, tile sort, ranges, blend, num_rendered read-back)"}
+
     # the side measurements below run on one view and need the memory of the batch's problem back
     # (at configs[4], 5M Gaussians x 32 4K views, that is ~100 GB)
     n_views_local = len(prob.views)
@@ -235,6 +273,7 @@ def main():
     # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
     # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
     fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
+    c0_gpu = time_config0_gpu(device) if rank == 0 else None
 
     # ---------------- BASELINE configs[2] as train_jvp.py runs it: one full LM step (loss, J^T b, CGLS with
     # 10 iterations and the reference's residual monitor, 7-point line search on the validation view)
@@ -253,20 +292,28 @@ def main():
         cm = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu")
         cc = orbit_cameras(1, W, H, seed=1)[0]
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
-        r = cpu_matvec_rate(cm, cc, torch.zeros(3), n_tiles=args.cpu_tiles, repeats=2, threads=threads)
+        r = cpu_matvec_rate(cm, cc, torch.zeros(3), n_tiles=args.cpu_tiles, repeats=3, threads=threads)
+        from oracle.cpu_baseline import cpu_config0_times, host_info
+        c0 = cpu_config0_times(repeats=5, threads=threads)
         cpu = {"value": 1.0 / r["matvec_s"], "unit": "view-matvec/s", "cores": r["threads"], "kind": "port",
                "sample": (f"oracle/torch_raster.py (PyTorch CPU, {r['threads']} threads, {r['cpu_model']}): "
                           f"all {args.P} Gaussians through preprocess+binning with forward-AD and autograd, "
                           f"blend JVP+VJP on {r['n_tiles']} of {r['ntiles']} tiles spread over the 1080p frame, "
-                          f"scaled to the full frame; t_pre={r['t_pre']:.2f}s t_sub={r['t_sub']:.2f}s"),
-               "raster_mpix_s": W * H / r["forward_s"] / 1e6}
+                          f"scaled to the full frame (median of 3); t_pre={r['t_pre']:.2f}s t_sub={r['t_sub']:.2f}s"),
+               "raster_mpix_s": W * H / r["forward_s"] / 1e6,
+               "host": host_info(),
+               "threads_note": "OMP_NUM_THREADS threads (the GPU box's CPU share for this job; os.cpu_count() "
+                               "reports the whole machine)",
+               "configs0": dict(c0, config="BASELINE configs[0]: 2000 Gaussians SH0, one 256x256 view, oracle "
+                                           "forward / JVP / VJP, 1 warm-up + median of 5, no extrapolation")}
 
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": n_views * args.steps / t_cg,
             "unit": "view-matvec/s (one (J^T J + D) application per 1080p view, 1M Gaussians)",
-            "n_gpus": world_size, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world_size, "ranks": dist.get_world_size() if world_size > 1 else 1,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
@@ -285,9 +332,16 @@ def main():
             "stage_ms": {"tangent_preprocess": tangent_ms, "render_matvec": render_ms, "gather_backward": gather_ms},
             "roofline": {"bound": "hbm", "kernel": "k_render_matvec", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms},
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms,
+                         "frac_visited": alg_visited / (render_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "alg_bytes_visited": alg_visited,
+                         "note": "168 B per list entry + 20 B per pixel; frac_visited counts only the entries "
+                                 "a pixel of their tile can blend (sum over tiles of max n_contrib)"},
+            "raster_roofline": raster_roofline,
+            "tile_stats": ts,
             "cpu_baseline": cpu,
             "raster_fwd_bwd": fb,
+            "configs0_gpu": c0_gpu,
             "lm_step": lm,
             "ssim_cg": ssim,
             "first_order": fo,
@@ -297,6 +351,72 @@ def main():
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def tile_stats(vr, P):
+    """N_dup, visited entries (sum over tiles of the max n_contrib of their pixels) and the mean n_contrib per
+    pixel of one preprocessed view (SURVEY 8(d) asks for N_dup and the mean blended count per pixel)."""
+    from gslm import _lib
+    H, W = vr.H, vr.W
+    nc = torch.zeros(H * W, dtype=torch.int32, device=vr.device)
+    _lib.check(_lib.lib.gslm_inspect(vr.geom.data_ptr(), P, vr.binning.data_ptr(), vr.N, H, W, vr.image.data_ptr(),
+                                     None, None, None, None, nc.data_ptr(), None, _lib.stream_handle(vr.device)))
+    gy, gx = (H + 15) // 16, (W + 15) // 16
+    pad = torch.zeros(gy * 16, gx * 16, dtype=torch.int32, device=vr.device)
+    pad[:H, :W] = nc.view(H, W)
+    per_tile = pad.view(gy, 16, gx, 16).amax(dim=(1, 3))
+    return {"num_rendered": int(vr.N), "visited_entries": int(per_tile.sum()),
+            "visited_frac": float(per_tile.sum()) / max(int(vr.N), 1),
+            "mean_n_contrib_per_pixel": float(nc.double().mean()), "tiles": gx * gy}
+
+
+def time_config0_gpu(device, reps=20):
+    """BASELINE configs[0] on the GPU through the drop-in rasterizer (forward, forward-mode JVP, VJP): 2000 Gaussians,
+    SH 0, one 256x256 view, median of `reps` host-timed calls (each includes the num_rendered read-back)."""
+    import torch.autograd.forward_ad as fwAD
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    m = synthetic_gaussians(2000, 0, seed=0, s0=0.005, device="cpu").to(device)
+    cam = orbit_cameras(1, 256, 256, seed=1)[0].to(device)
+    st = GaussianRasterizationSettings(
+        image_height=256, image_width=256, tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+        bg=torch.zeros(3, device=device), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=0, campos=cam.camera_center, prefiltered=False, debug=False,
+        antialiasing=False)
+    rast = GaussianRasterizer(st)
+    a = {"means3D": m.get_xyz.detach(), "opacities": m.get_opacity.detach(), "scales": m.get_scaling.detach(),
+         "rotations": m.get_rotation.detach(), "shs": m.get_features.detach().contiguous()}
+    g3 = torch.Generator().manual_seed(3)
+    tang = {k: torch.randn(v.shape, generator=g3).to(device) for k, v in a.items()}
+    dcol = torch.randn(3, 256, 256, generator=torch.Generator().manual_seed(4)).to(device)
+    m2 = torch.zeros_like(a["means3D"])
+
+    def fwd():
+        with torch.no_grad():
+            rast(means2D=m2, **a)
+
+    def jvp():
+        with torch.no_grad(), fwAD.dual_level():
+            fwAD.unpack_dual(rast(means2D=m2, **{k: fwAD.make_dual(v, tang[k]) for k, v in a.items()})[0]).tangent
+
+    def vjp():
+        leaves = {k: v.clone().requires_grad_(True) for k, v in a.items()}
+        (rast(means2D=m2, **leaves)[0] * dcol).sum().backward()
+
+    out = {"config": "BASELINE configs[0] on the GPU: 2000 Gaussians SH0, one 256x256 view, drop-in rasterizer, "
+                     "median of host-timed calls"}
+    for name, fn in (("forward", fwd), ("jvp", jvp), ("vjp", vjp)):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        out[name + "_ms"] = 1e3 * sorted(ts)[len(ts) // 2]
+    return out
 
 
 def _events_ms(fn, reps):

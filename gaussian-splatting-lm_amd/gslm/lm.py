@@ -562,17 +562,22 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
                          verbose=verbose)
     s = prob.expand(s)
+    del prob
     val = LMProblem(model, val_cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
+    # train_jvp.py:262-279: alpha = 2, 1, ..., 1/16 on the validation views, keep the best, step to it
     alpha = 2.0
     best_alpha, best_loss = alpha, math.inf
-    update_params(model, prob.full_layout, s, alpha)
+    trace = []
+    update_params(model, val.full_layout, s, alpha)
     for _ in range(6):
         vl = float(val.evaluate())
+        trace.append((alpha, vl))
         if vl < best_loss:
             best_loss, best_alpha = vl, alpha
         new_alpha = alpha * 0.5
-        update_params(model, prob.full_layout, s, new_alpha - alpha)
+        update_params(model, val.full_layout, s, new_alpha - alpha)
         alpha = new_alpha
-    update_params(model, prob.full_layout, s, best_alpha - alpha)
+    update_params(model, val.full_layout, s, best_alpha - alpha)
     final = float(val.evaluate())
-    return dict(start_loss=float(start_loss), final_val_loss=final, best_alpha=best_alpha, cg=info, step=s)
+    return dict(start_loss=float(start_loss), final_val_loss=final, best_alpha=best_alpha, cg=info, step=s,
+                trace=trace)

@@ -111,6 +111,61 @@ def render(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, separate_
             "visibility_filter": (radii > 0).nonzero(), "radii": radii, "depth": depth_image}
 
 
+def batch_render(viewpoint_cameras, pc, pipe, bg_color, scaling_modifier=1.0, separate_sh=False, override_color=None,
+                 use_trained_exp=False):
+    """gaussian_renderer/batch_render.py:8-135: the batch settings, BatchGaussianRasterizer, clamp and the dict
+    (render [B,3,maxH,maxW], viewspace_points, visibility_filter of radii.max(0), max_radii, depth, viewcount)."""
+    from diff_gaussian_rasterization.batch_render import BatchGaussianRasterizationSettings, BatchGaussianRasterizer
+    from gslm.model import eval_sh
+    if use_trained_exp:
+        raise NotImplementedError("Batch exposure not implemented yet")  # batch_render.py:117-118
+    dev = pc.get_xyz.device
+    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True, device=dev) + 0
+    try:
+        screenspace_points.retain_grad()
+    except RuntimeError:
+        pass
+    cams = list(viewpoint_cameras)
+    settings = BatchGaussianRasterizationSettings(
+        batch_size=len(cams), image_heights=[int(c.image_height) for c in cams],
+        image_widths=[int(c.image_width) for c in cams], tanfovxs=[math.tan(c.FoVx * 0.5) for c in cams],
+        tanfovys=[math.tan(c.FoVy * 0.5) for c in cams], bg=bg_color, scale_modifier=scaling_modifier,
+        viewmatrices=[c.world_view_transform for c in cams], projmatrices=[c.full_proj_transform for c in cams],
+        sh_degree=pc.active_sh_degree, camposes=[c.camera_center for c in cams], prefiltered=False, debug=pipe.debug,
+        antialiasing=pipe.antialiasing)
+    rasterizer = BatchGaussianRasterizer(batch_raster_settings=settings)
+    scales = rotations = cov3D_precomp = None
+    if pipe.compute_cov3D_python:
+        cov3D_precomp = pc.get_covariance(scaling_modifier)
+    else:
+        scales, rotations = pc.get_scaling, pc.get_rotation
+    shs = colors_precomp = dc = None
+    if override_color is None:
+        if pipe.convert_SHs_python:
+            # the reference's branch reads an undefined `viewpoint_camera` here (batch_render.py:77); one set of
+            # colours for the whole batch needs one centre -- the first camera's
+            shs_view = pc.get_features.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
+            dir_pp = pc.get_xyz - cams[0].camera_center.repeat(pc.get_features.shape[0], 1)
+            dir_pp_normalized = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+            colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dir_pp_normalized) + 0.5, 0.0)
+        elif separate_sh:
+            dc, shs = pc.get_features_dc, pc.get_features_rest
+        else:
+            shs = pc.get_features
+    else:
+        colors_precomp = override_color
+    kw = dict(means3D=pc.get_xyz, means2D=screenspace_points, shs=shs, colors_precomp=colors_precomp,
+              opacities=pc.get_opacity, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp)
+    if separate_sh:
+        kw["dc"] = dc
+    rendered_image, radii, depth_image = rasterizer(**kw)
+    rendered_image = rendered_image.clamp(0, 1)
+    max_radii = radii.max(dim=0).values
+    return {"render": rendered_image, "viewspace_points": screenspace_points,
+            "visibility_filter": (max_radii > 0).nonzero(), "max_radii": max_radii, "depth": depth_image,
+            "viewcount": (radii > 0).sum(dim=0)}
+
+
 class Trainer:
     """State of train.py:training() between iterations (model, cameras, background, view stack)."""
 

@@ -68,13 +68,13 @@ def cpu_matvec_rate(model, cam, bg, n_tiles=32, repeats=1, threads=None):
     tangents = [torch.randn(t.shape, generator=g) for t in
                 (model._features_dc, model._features_rest, model._scaling, model._rotation, model._opacity)]
 
-    def timed(fn):
-        best = float("inf")
+    def timed(fn):  # median of `repeats` runs
+        ts = []
         for _ in range(repeats):
             t0 = time.perf_counter()
             fn()
-            best = min(best, time.perf_counter() - t0)
-        return best
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
 
     t_pre = timed(lambda: _matvec_once(model, cam, bg, set(), tangents))
     t_sub = timed(lambda: _matvec_once(model, cam, bg, subset, tangents))
@@ -96,3 +96,62 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def cpu_config0_times(repeats=5, threads=None):
+    """BASELINE.json configs[0] (BASELINE.md "CPU baseline plan"): 2k synthetic Gaussians, SH 0, one 256x256 view,
+    on the oracle renderer with no sampling or extrapolation: forward, JVP (forward-AD over every activated input,
+    the tangent seed 3) and VJP (autograd with dL/dcolor ~ N(0,1), seed 4); 1 warm-up then the median of
+    `repeats` timed runs of each.  Returns seconds per call and the thread count."""
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    if threads:
+        torch.set_num_threads(threads)
+    model = synthetic_gaussians(2000, 0, seed=0, s0=0.005)
+    cam = orbit_cameras(1, 256, 256, seed=1)[0]
+    st = tr.settings_from_camera(cam, torch.zeros(3), 0)
+    with torch.no_grad():
+        a = dict(means3D=model.get_xyz.detach().clone(), opacities=model.get_opacity.detach().clone(),
+                 scales=model.get_scaling.detach().clone(), rotations=model.get_rotation.detach().clone(),
+                 shs=model.get_features.detach().clone())
+    g3 = torch.Generator().manual_seed(3)
+    tang = {k: torch.randn(v.shape, generator=g3) for k, v in a.items()}
+    dcol = torch.randn(3, 256, 256, generator=torch.Generator().manual_seed(4))
+
+    def call(inp):
+        return tr.rasterize(inp["means3D"], torch.zeros_like(a["means3D"]), inp["opacities"], st, shs=inp["shs"],
+                            scales=inp["scales"], rotations=inp["rotations"])[0]
+
+    def fwd():
+        with torch.no_grad():
+            call(a)
+
+    def jvp():
+        with torch.no_grad(), fwAD.dual_level():
+            fwAD.unpack_dual(call({k: fwAD.make_dual(v, tang[k]) for k, v in a.items()})).tangent
+
+    def vjp():
+        leaves = {k: v.clone().requires_grad_(True) for k, v in a.items()}
+        (call(leaves) * dcol).sum().backward()
+
+    out = {}
+    for name, fn in (("forward", fwd), ("jvp", jvp), ("vjp", vjp)):
+        fn()
+        ts = []
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        out[name + "_s"] = sorted(ts)[len(ts) // 2]
+    out["threads"] = torch.get_num_threads()
+    return out
+
+
+def host_info():
+    """os.cpu_count(), the CPU model and the cores this process may run on (the GPU box's CPU share)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": _cpu_model(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}

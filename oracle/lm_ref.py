@@ -172,3 +172,22 @@ def cgls_ref(op, g, max_iter, restart_iter, tol=1e-10, atol=0.0):
         if stop:
             break
     return x
+
+
+def line_search_ref(apply_step, val_loss, alpha=2.0, halvings=6):
+    """The backtracking line search of train_jvp.py:262-279, restated (train_jvp.py is a script and cannot be
+    imported).  apply_step(a) performs gaussians.update_step(a * s); val_loss() evaluates the validation batch's
+    loss_scalar.  The model is left at best_alpha * s.  Returns (best_alpha, final_val_loss, [(alpha, loss)])."""
+    best_alpha, best_loss = alpha, math.inf
+    apply_step(alpha)                                # gaussians.update_step(alpha * s)        :266
+    trace = []
+    for _ in range(halvings):                        # for i in range(6)                       :267
+        vl = float(val_loss())
+        trace.append((alpha, vl))
+        if vl < best_loss:                           # strict: the first (largest) alpha wins ties
+            best_loss, best_alpha = vl, alpha
+        new_alpha = alpha * 0.5
+        apply_step(new_alpha - alpha)                # update_step(alpha_update * s)           :274-275
+        alpha = new_alpha
+    apply_step(best_alpha - alpha)                   # update_step(best_update * s)            :277-278
+    return best_alpha, float(val_loss()), trace      # val_loss = val_loss_func().loss_scalar  :279

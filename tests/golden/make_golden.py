@@ -21,6 +21,10 @@ What is pinned by the *reference's code* (imported from /root/reference, never c
   * solver_ssim_golden.npz  the same solver run with the disable_ssim=False residual
                        (solver/batch_training_loss.py:18-30, restated around the reference's own
                        l1_loss_per_pixel / ssim_per_pixel): loss, J^T b, (J^T J + D) v, 10-iteration CGLS
+  * lm_step_golden.npz one LM step of train_jvp.py:237-279: the reference's cgls_damped (schedule 2 x 1) on the
+                       solver scene, then the restated backtracking line search (oracle/lm_ref.py) on three
+                       validation views stepping the model by the reference's GaussianModelState arithmetic:
+                       best_alpha, the (alpha, val loss) trace, the final val loss and the stepped parameters
   * train_golden.npz   the first-order step: utils/general_utils.py get_expon_lr_func
                        at the schedules GaussianModel.training_setup builds (scene/gaussian_model.py:293-301,
                        OptimizationParams defaults of arguments/__init__.py:76-90), and the trajectory of
@@ -290,6 +294,64 @@ def solver_golden():
     np.savez(os.path.join(HERE, "solver_golden.npz"), **out)
 
 
+LM_VAL_VIEWS = 3  # validation cameras of the line-search golden (seed 4), GT from the same perturbed model
+
+
+def lm_step_golden():
+    """One LM step as train_jvp.py:237-279 runs it: the reference's LinearSolverFunctions + cgls_damped (reference
+    schedule max_iter=2, restart_iter=1, and 10 x 10) on the solver scene, then the backtracking line search (restated in
+    oracle/lm_ref.py:line_search_ref -- train_jvp.py is a script) on separate validation views, stepping the model
+    with the reference's own GaussianModelState arithmetic (gaussians.update_step(alpha * s)).
+    Pins best_alpha, every (alpha, val loss) pair, the final val loss and the stepped parameters."""
+    from oracle.lm_ref import line_search_ref
+    with reference_on_path():
+        from solver.conjugate_gradient import cgls_damped
+        from solver.gaussian_model_state import GaussianModelDampMatrix, GaussianModelParamGroupMask
+        from solver.loss_image_state import BatchLossImageState
+        from solver.solver_functions import LinearSolverFunctions
+    model, cams = solver_scene()
+    sc = SOLVER_SCENE
+    val_cams = orbit_cameras(LM_VAL_VIEWS, sc["W"], sc["H"], seed=4)
+    g = torch.Generator().manual_seed(2)
+    pert = synthetic_gaussians(sc["P"], sc["D"], seed=0, s0=sc["s0"], n_cams=sc["views"])
+    with torch.no_grad():
+        pert._features_dc += 0.01 * torch.randn(pert._features_dc.shape, generator=g)
+        pert._opacity += 0.01 * torch.randn(pert._opacity.shape, generator=g)
+        pert._scaling += 0.01 * torch.randn(pert._scaling.shape, generator=g)
+        for c in val_cams:
+            c.original_image = tr.render_model(pert, c, torch.zeros(3))[0].detach().clone()
+    loss_func = partial(oracle_batch_loss, BatchLossImageState=BatchLossImageState)
+    param_mask = GaussianModelParamGroupMask(mask_xyz=True)
+    damp = GaussianModelDampMatrix(xyz_damp=5e2, features_dc_damp=5e-2, features_rest_damp=5e-2, scaling_damp=5e-2,
+                                   rotation_damp=5e-2, opacity_damp=5e-2, exposure_damp=1e1)
+    out = {}
+    base = [t.detach().clone() for t in model.params()]
+    for tag, (mi, ri) in {"ref": (2, 1), "ten": (10, 10)}.items():
+        model.set_params(*base)
+        st = LinearSolverFunctions(loss_func, model, cams, batch_size=20, param_mask=param_mask)
+        out[f"{tag}_start_loss"] = np.array(float(st.evaluate_loss().loss_scalar))
+        with torch.no_grad():
+            b = -1 * st.loss
+            s = cgls_damped(matvec=st.matvec, matvec_T=st.matvec_T, dot=st.dot, saxpy=st.saxpy, b=b,
+                            x0=st.get_initial_solution(), damp=damp, tol=1e-10, atol=0.0, max_iter=mi,
+                            restart_iter=ri, verbose=False)
+            del st
+            out[f"{tag}_s"] = s.as_1d_tensor().detach().numpy()
+            val_loss_func = partial(loss_func, gaussians=model, viewpoint_cams=val_cams)
+            best_alpha, final, trace = line_search_ref(lambda a: model.update_step(a * s),
+                                                       lambda: val_loss_func().loss_scalar)
+        out[f"{tag}_best_alpha"] = np.array(best_alpha)
+        out[f"{tag}_final_val_loss"] = np.array(final)
+        out[f"{tag}_trace_alpha"] = np.array([a for a, _ in trace])
+        out[f"{tag}_trace_loss"] = np.array([v for _, v in trace])
+        for k, t in zip(("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity", "exposure"),
+                        model.params()):
+            out[f"{tag}_out_{k}"] = t.detach().numpy()
+    for i, c in enumerate(val_cams):
+        out[f"val_gt{i}"] = c.original_image.numpy()
+    np.savez(os.path.join(HERE, "lm_step_golden.npz"), **out)
+
+
 TRAIN_STEPS = [0, 1, 2, 10, 100, 500, 1000, 7000, 15000, 29999, 30000, 45000]
 ADAM_P = 37  # odd: every group's float count is exercised with a ragged float4 tail
 
@@ -360,4 +422,5 @@ if __name__ == "__main__":
     solver_ssim_golden()
     train_golden()
     raster_fixture()
+    lm_step_golden()
     print("golden fixtures written to", HERE)

@@ -31,17 +31,17 @@ def activated(model):
                     shs=model.get_features.detach().clone())
 
 
-def oracle_settings(cam, D, bg=None):
+def oracle_settings(cam, D, bg=None, scale_modifier=1.0, antialiasing=False):
     bg = torch.zeros(3) if bg is None else bg
-    return tr.settings_from_camera(cam, bg, D)
+    return tr.settings_from_camera(cam, bg, D, scale_modifier=scale_modifier, antialiasing=antialiasing)
 
 
-def gpu_settings(cam, D, bg=None, device="cuda"):
+def gpu_settings(cam, D, bg=None, device="cuda", scale_modifier=1.0, antialiasing=False):
     from diff_gaussian_rasterization import GaussianRasterizationSettings
     bg = torch.zeros(3) if bg is None else bg
     return GaussianRasterizationSettings(
         image_height=int(cam.image_height), image_width=int(cam.image_width),
         tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5), bg=bg.to(device),
-        scale_modifier=1.0, viewmatrix=cam.world_view_transform.to(device),
+        scale_modifier=float(scale_modifier), viewmatrix=cam.world_view_transform.to(device),
         projmatrix=cam.full_proj_transform.to(device), sh_degree=D, campos=cam.camera_center.to(device),
-        prefiltered=False, debug=False, antialiasing=False)
+        prefiltered=False, debug=False, antialiasing=bool(antialiasing))

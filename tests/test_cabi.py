@@ -87,3 +87,16 @@ def test_rasterizer_argument_validation():
         r(means3D=x, means2D=x, opacities=torch.zeros(4, 1), scales=x, rotations=torch.zeros(4, 4))
     with pytest.raises(Exception, match="scale/rotation pair"):
         r(means3D=x, means2D=x, opacities=torch.zeros(4, 1), colors_precomp=x)
+
+
+def test_simple_knn_module_binds_the_hip_kernel():
+    """scene/gaussian_model.py:22 imports `from simple_knn._C import distCUDA2` at module load: the build ships
+    that module, bound to the HIP kernel (gslm.knn), and it rejects host tensors instead of computing on the CPU."""
+    import torch
+    from simple_knn._C import distCUDA2
+    from gslm import knn
+    assert distCUDA2 is knn.distCUDA2
+    with pytest.raises(ValueError, match="GPU tensor"):
+        distCUDA2(torch.zeros(8, 3))
+    with pytest.raises(ValueError, match=r"\[N, 3\]"):
+        distCUDA2(torch.zeros(8, 2))

@@ -52,3 +52,12 @@ def test_create_from_pcd_scales():
     assert torch.allclose(m.get_opacity.detach().cpu(), torch.full((5000, 1), 0.1), atol=1e-6)
     assert m._exposure.shape == (2, 3, 4)
     assert distCUDA2(torch.from_numpy(pts).cuda()).shape == (5000,)
+
+
+def test_simple_knn_module_matches_oracle():
+    """The reference's import path (scene/gaussian_model.py:22, :249) reaches the same kernel."""
+    from simple_knn._C import distCUDA2
+    p = _clouds()["blobs"]
+    got = torch.clamp_min(distCUDA2(torch.from_numpy(p).float().cuda()), 0.0000001).cpu().numpy()
+    ref = np.maximum(dist_cuda2_ref(p), 0.0000001)
+    assert np.abs(got - ref).max() <= 1e-6 * np.abs(ref).max()

@@ -4,8 +4,9 @@ tests/golden/solver_golden.npz was produced by the reference's own cgls_damped /
 LinearSolverFunctions / GaussianModelState (imported from /root/reference, make_golden.py) around
 the CPU oracle renderer.  Here the same scene runs through libgslm (raw-parameter preprocess,
 fused JVP->VJP matvec, gather-sum backward, device scalars) and must reproduce:
-  loss (rel 1e-5), J^T b and (J^T J + D) v (1e-4 of the vector's max), and the CGLS solutions of
-  the reference schedule (max_iter=2, restart_iter=1) and of 10 iterations (rel 2e-3 in norm).
+  loss (rel 1e-5), J^T b and (J^T J + D) v (1e-5 of the vector's max), and the CGLS solutions of
+  the reference schedule (max_iter=2, restart_iter=1, rel 1e-5 in norm) and of 10 iterations (rel 1e-4).
+  The CPU oracle itself reaches 1.6e-7 / 1.3e-6 on the same goldens (tests/test_oracle_golden.py).
 """
 import os
 
@@ -35,6 +36,11 @@ def _load():
     return d, m, cams
 
 
+def _err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+
+
 def _close(a, b, tol):
     a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
     return np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-12)
@@ -47,14 +53,14 @@ def test_loss_rhs_matvec_match_reference_solver():
     loss = float(prob.evaluate())
     assert abs(loss - float(d["loss"])) <= 1e-5 * float(d["loss"])
     g = prob.rhs(prob.zeros())
-    assert _close(g.cpu().numpy(), d["Jtb"], 1e-4)
+    assert _close(g.cpu().numpy(), d["Jtb"], 1e-5), _err(g.cpu().numpy(), d["Jtb"])
     v = torch.from_numpy(d["v"]).cuda()
     y = prob.matvec(v, prob.zeros())
-    assert _close(y.cpu().numpy(), d["Av"], 1e-4)
+    assert _close(y.cpu().numpy(), d["Av"], 1e-5), _err(y.cpu().numpy(), d["Av"])
 
 
-@pytest.mark.parametrize("sched,key", [((2, 1), "x_ref_schedule"), ((10, 10), "x_ten")])
-def test_cgls_matches_reference_schedule(sched, key):
+@pytest.mark.parametrize("sched,key,tol", [((2, 1), "x_ref_schedule", 1e-5), ((10, 10), "x_ten", 1e-4)])
+def test_cgls_matches_reference_schedule(sched, key, tol):
     from gslm.lm import LMProblem, cgls_fused
     d, m, cams = _load()
     prob = LMProblem(m, cams, torch.zeros(3))
@@ -63,7 +69,7 @@ def test_cgls_matches_reference_schedule(sched, key):
     x, info = cgls_fused(prob, g, max_iter=sched[0], restart_iter=sched[1], check_every=True)
     ref = d[key]
     err = np.linalg.norm(x.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref)
-    assert err < 2e-3, err
+    assert err < tol, err
 
 
 def test_cg_nocheck_matches_checked():

@@ -141,3 +141,30 @@ def test_oracle_ssim_lm_algebra_matches_reference_solver():
     x = cgls_ref(op, g, 10, 10)
     err = np.linalg.norm(x.numpy().astype(np.float64) - d["x_ten"]) / np.linalg.norm(d["x_ten"])
     assert err < 1e-3, err
+
+
+@pytest.mark.parametrize("tag", ["ref", "ten"])
+def test_oracle_line_search_matches_lm_step_golden(tag):
+    """oracle/lm_ref.py:line_search_ref (train_jvp.py:262-279) with the oracle's flat-vector update on the golden's
+    CG step reproduces the golden's (alpha, val loss) trace, best_alpha, final loss and stepped parameters."""
+    from gslm.lm import update_params
+    from gslm.params import ParamLayout
+    from oracle.lm_ref import OracleLMProblem, line_search_ref
+    d, L = _g("solver_golden.npz"), _g("lm_step_golden.npz")
+    P, D, W, H, s0, nv = (int(x) if i != 4 else x for i, x in enumerate(d["scene"]))
+    names = ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity", "exposure")
+    m = GaussianModel(D)
+    m.set_params(*(torch.from_numpy(d[f"in_{k}"]) for k in names))
+    m.active_sh_degree = D
+    nval = sum(1 for k in L.files if k.startswith("val_gt"))
+    val = orbit_cameras(nval, W, H, seed=4, images=[torch.from_numpy(L[f"val_gt{i}"]) for i in range(nval)])
+    layout = ParamLayout(P, (D + 1) ** 2, m._exposure.shape[0])
+    s = torch.from_numpy(L[f"{tag}_s"])
+    op = OracleLMProblem(m, val, torch.zeros(3))
+    best, final, trace = line_search_ref(lambda a: update_params(m, layout, s, a), lambda: float(op.evaluate()))
+    assert best == float(L[f"{tag}_best_alpha"])
+    assert [a for a, _ in trace] == list(L[f"{tag}_trace_alpha"])
+    assert np.allclose([v for _, v in trace], L[f"{tag}_trace_loss"], rtol=1e-6, atol=0)
+    assert abs(final - float(L[f"{tag}_final_val_loss"])) <= 1e-6 * float(L[f"{tag}_final_val_loss"])
+    for k, t in zip(names, m.params()):
+        assert np.allclose(t.detach().numpy(), L[f"{tag}_out_{k}"], rtol=0, atol=1e-6), k
