@@ -187,29 +187,31 @@ def main():
     mpix = n_views * W * H * fsteps / t_fwd / 1e6
 
     # ---------------- roofline of the dominant kernel: the fused JVP->VJP tile pass (k_render_matvec)
-    vr = prob.views[0]
-    vs = prob.layout.grads_struct(x)
-    ys = prob.layout.grads_struct(prob.zeros(), accumulate=True)
+    loc = getattr(prob, "local", prob)  # the rank's own LMProblem (full P) under a sharded operator
+    vr = loc.views[0]
+    xv = prob.gather_full(x) if getattr(prob, "exchange", None) == "gaussian" else x
+    vs = loc.layout.grads_struct(xv)
+    ys = loc.layout.grads_struct(loc.zeros(), accumulate=True)
     lib, check = _lib.lib, _lib.check
 
     def stage(mask):
         opts = _lib.GslmMatvecOpts()
         opts.stages = mask | (8 if mask == 4 else 0)  # the gather in its CG form: overwrite + D v
-        opts.flags = (1 if mask == 2 else 0) | prob.mv_flags  # GSLM_MV_TAIL_CLEAN: as inside the CG loop
-        opts.damp7 = prob._damps if mask == 4 else None
+        opts.flags = (1 if mask == 2 else 0) | loc.mv_flags  # GSLM_MV_TAIL_CLEAN: as inside the CG loop
+        opts.damp7 = loc._damps if mask == 4 else None
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
-                                      prob.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                      loc.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                       vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
-                                      ctypes.byref(ys), ctypes.byref(opts), prob.stream))
+                                      ctypes.byref(ys), ctypes.byref(opts), loc.stream))
 
     stage(1)
     opts0 = _lib.GslmMatvecOpts()
     opts0.stages = 2  # RENDER once with the tail rows written: the state every CG iteration after the first sees
-    opts0.flags = prob.mv_flags
-    check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs), prob.weights[0].data_ptr(),
+    opts0.flags = loc.mv_flags
+    check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs), loc.weights[0].data_ptr(),
                                   1, vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                   vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts0),
-                                  prob.stream))
+                                  loc.stream))
     stage(2)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = max(args.steps, 5)
@@ -264,10 +266,10 @@ def main():
 
     # the side measurements below run on one view and need the memory of the batch's problem back
     # (at configs[4], 5M Gaussians x 32 4K views, that is ~100 GB)
-    n_views_local = len(prob.views)
+    n_views_local = len(loc.views)
     sh_proj = prob.layout.rest_projected
     exchange = prob.exchange if world_size > 1 else "none"
-    del prob, vr, vs, ys, x, g
+    del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
 
     # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward

@@ -90,14 +90,9 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
 // ------------------------------------------------------------------ launcher
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                        const ScratchBufs& sb, const XpbyK* xp, hipStream_t s) {
-  if (g.P == 0) {
-    if (xp && xp->tail_p) {
-      set_error("internal: fused xpby with P = 0");
-      return GSLM_ERR_INVALID;
-    }
-    return GSLM_OK;
-  }
-  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  // P = 0 with a fused direction update: one block still applies the flat tail's update (block_xpby)
+  if (g.P == 0 && !(xp && xp->tail_p)) return GSLM_OK;
+  const unsigned nb = (unsigned)((g.P + 255) / 256) + (g.P == 0 ? 1u : 0u);
   XpbyK none{};
   const XpbyK& x = xp ? *xp : none;
   if (xp) {
@@ -166,13 +161,7 @@ int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const 
     set_error("tangent_views: 1..16 views per call");
     return GSLM_ERR_INVALID;
   }
-  if (g.P == 0) {
-    if (xp && xp->tail_p) {
-      set_error("tangent_views: fused xpby with P = 0");
-      return GSLM_ERR_INVALID;
-    }
-    return GSLM_OK;
-  }
+  if (g.P == 0 && !(xp && xp->tail_p)) return GSLM_OK;  // an empty shard with a tail: one block updates it
   if (xp && t.rest && (t.rest != xp->p[2] || t.rest_stride != xp->w[2])) {
     set_error("internal: fused xpby expects the tangent's SH-rest group to be p's");
     return GSLM_ERR_INVALID;
@@ -180,7 +169,7 @@ int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const 
   ViewsK vs;
   for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
   vs.n = nviews;
-  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const unsigned nb = (unsigned)((g.P + 255) / 256) + (g.P == 0 ? 1u : 0u);
   const size_t lds = t.rest ? (size_t)256 * t.rest_stride * sizeof(float) : 0;
   XpbyK none{};
   float4* o = reinterpret_cast<float4*>(out);

@@ -466,6 +466,13 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     # the update kernel then streams s and q only; the iterates are bitwise those of the undeferred loop.
     defer = not check_every and callback is None
     pend = None  # (alpha_num, alpha_den) of a deferred x update not yet applied
+    # Gaussian-sharded operators (gslm.parallel.GaussianShardedOperator) hold a shard of every vector: each
+    # dot / update pass leaves a per-shard partial that is summed over the ranks before it is used
+    red = getattr(prob, "allreduce_scalars", None)
+
+    def reduce(*slots):
+        if red is not None:
+            red(sc, slots)
 
     def flush():
         nonlocal pend
@@ -484,6 +491,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             torch.sub(g, q, out=s)
         p.copy_(s)
         prob.dot(s[lo:], s[lo:], ptr(GAM))
+        reduce(GAM)
         stop = False
         pre = None
         for _ in range(restart_iter):
@@ -494,6 +502,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 pend = None
             if not prob.matvec_dot(p, q, ptr(DEL), pre=full):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
+            reduce(DEL)
             if check_every and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
@@ -504,13 +513,16 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 check(lib.gslm_cg_update_monitor(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s), off(g),
                                                  prob.dot_scratch.data_ptr(), prob.dot_scratch.numel() * 8,
                                                  ptr(GAMN), ptr(XG), ptr(XS), st))
+                reduce(GAMN, XG, XS)
             elif defer:
                 check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), None, off(s),
                                          prob.dot_scratch.data_ptr(), ptr(GAMN), st))
                 pend = (ptr(GAM), ptr(DEL))  # alpha = gamma / delta, read before either slot is rewritten
+                reduce(GAMN)
             else:
                 check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s),
                                          prob.dot_scratch.data_ptr(), ptr(GAMN), st))
+                reduce(GAMN)
             # beta = gamma' / gamma; after the slot swap below these are the GAM / GAMN slots
             pre = (s, ptr(GAMN), ptr(GAM))
             if check_every:

@@ -19,8 +19,13 @@ stay consistent without a further broadcast.
 `ShardedOperator` wraps any per-rank operator with the LMProblem protocol (gslm.lm.LMProblem on
 the GPU, oracle.lm_ref.OracleLMProblem in the CPU tests; the screen exchange needs the former).
 """
+import ctypes
+import math
+
 import torch
 import torch.distributed as dist
+
+from gslm.params import GROUPS, ParamLayout
 
 
 def world():
@@ -142,8 +147,340 @@ class ShardedOperator:
 
 def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto", **kw):
     """LMProblem over this rank's views, wrapped for the cross-rank reductions.  all_cams (every
-    rank's views, in rank order) enables the screen exchange."""
+    rank's views, in rank order) enables the screen and Gaussian-sharded exchanges.
+
+    exchange: "gaussian" (GaussianShardedOperator: CG vectors sharded by Gaussian, two all-to-alls per
+    product), "screen" / "allreduce" (ShardedOperator: vectors replicated), or "auto" -- "gaussian" when
+    several ranks render the same number of views each with the disable_ssim residual, else
+    ShardedOperator's own choice."""
     from gslm.lm import LMProblem
-    if world()[1] > 1 or (all_cams is not None and len(all_cams) > 1):
+    rank, n = world()
+    if n > 1 or (all_cams is not None and len(all_cams) > 1):
         kw["sh_projection"] = False  # the SH-rest span is one view's: the global batch has several
-    return ShardedOperator(LMProblem(model, cams, bg, **kw), group=group, all_cams=all_cams, exchange=exchange)
+    local = LMProblem(model, cams, bg, **kw)
+    if exchange == "auto" and n > 1 and all_cams is not None and len(cams) >= 1 and \
+            len(all_cams) == n * len(cams) and local.mask_xyz and not local.ssim:
+        exchange = "gaussian"
+    if exchange == "gaussian":
+        if local.ssim or not local.mask_xyz:
+            raise ValueError("the Gaussian-sharded exchange runs the disable_ssim product with xyz frozen")
+        return GaussianShardedOperator(local, group=group, all_cams=all_cams if all_cams is not None else cams)
+    return ShardedOperator(local, group=group, all_cams=all_cams, exchange=exchange)
+
+
+def _slice_gaussians(g, lo, hi):
+    """gslm_gaussians over Gaussians [lo, hi) of `g` (pointer offsets into the same leaves)."""
+    from gslm import _lib
+    out = _lib.GslmGaussians()
+    ctypes.pointer(out)[0] = g
+    out.P = hi - lo
+    for name, w in (("means3D", 3), ("opacities", 1), ("scales", 3), ("rotations", 4)):
+        p = getattr(g, name)
+        if p:
+            setattr(out, name, p + 4 * w * lo)
+    if g.sh_dc:
+        out.sh_dc = g.sh_dc + 4 * g.sh_dc_stride * lo
+    if g.sh_rest:
+        out.sh_rest = g.sh_rest + 4 * g.sh_rest_stride * lo
+    return out
+
+
+class GaussianShardedOperator:
+    """The Gaussian-sharded exchange (exchange "gaussian").
+
+    Views stay sharded as in ShardedOperator (rank r renders its block of `per` views), and in addition
+    the Gaussians are cut into n contiguous shards: rank r owns Gaussians [lo, hi) = [r S, (r+1) S) of
+    every CG vector (x, s, p, q and J^T b are shard-sized, `layout`) and the per-Gaussian work on them.
+    Per product (matvec_dot), with b = (k, t) running over every view (k-th view of rank t):
+      1. gslm_tangent_views: this shard's tangent render records for every view (the fused direction
+         update p = s + beta p [, x += alpha p] on the shard first) -> trec[k][t][S][12];
+      2. all_to_all per k: rank t receives every shard's records of its k-th view = a [P][12] table;
+      3. RENDER | SCREEN with opts.trec_in: the view's fused JVP -> VJP tile pass and row sums -> [P][8];
+      4. all_to_all per k: rank r receives the [S][8] slices of its shard from every view;
+      5. gslm_gather_screen over the shard, every view's chain, + D v, <v, y> partial.
+    The CG scalars are sums over shards: one small all-reduce each (DEL, GAMN [, monitor dots]) via
+    `allreduce_scalars`, which gslm.lm.cgls_fused calls.  A rank receives (48 + 32) (n - 1) / n bytes per
+    Gaussian per view instead of the screen all-gather's 32 (n - 1), and runs 1/n of the chains, gathers
+    and vector algebra.  J^T b and the loss are all-reduced once per LM step (full layout), then sliced.
+
+    With a per-rank operator that has no HIP views (oracle.lm_ref.OracleLMProblem in the CPU tests) the
+    product falls back to all-gather v -> local sum_b 2 J_b^T W_b J_b v -> all-reduce -> slice + D v on
+    the shard, which exercises the same shard layout, scalar reductions and gathers."""
+
+    exchange = "gaussian"
+
+    def __init__(self, local, group=None, all_cams=None):
+        self.local = local
+        self.group = group
+        self.rank, self.world_size = world()
+        full = local.layout
+        if getattr(full, "rest_projected", False):
+            raise ValueError("the Gaussian-sharded exchange runs on the full SH-rest layout")
+        self.full_layout = full
+        self.P = full.P
+        n = self.world_size
+        self.S = max(1, -(-self.P // n))
+        self.lo = min(self.rank * self.S, self.P)
+        self.hi = min(self.lo + self.S, self.P)
+        # the exposure group (zero in every LM iterate: J has no exposure column) lives on rank 0
+        self.layout = ParamLayout(self.hi - self.lo, full.K, full.n_exposure if self.rank == 0 else 0)
+        self.mask_xyz = getattr(local, "mask_xyz", True)
+        self.device = getattr(local, "device", "cpu")
+        self.kernel_path = hasattr(local, "views") and all_cams is not None
+        self.all_cams = all_cams
+        if self.kernel_path:
+            self.per = len(local.views)
+            if self.per < 1 or len(all_cams) != n * self.per:
+                raise ValueError("gaussian exchange: every rank renders the same number (>= 1) of views "
+                                 f"(got {self.per} here, {len(all_cams)} in all for {n} ranks)")
+            # view order b = k n + t (the k-th view of rank t): the all-to-all blocks of one k are contiguous
+            self.cams_kt = [all_cams[t * self.per + k] for k in range(self.per) for t in range(n)]
+            self.views_kt = local.views_for(self.cams_kt)
+            self._bufs = None
+        if hasattr(local, "_damps"):
+            self._damps = local._damps
+
+    def __getattr__(self, name):  # stream, dot_scratch, views, weights, model, ...
+        return getattr(self.local, name)
+
+    # ------------------------------------------------------------------ collectives
+    def _allreduce(self, t):
+        if self.world_size > 1:
+            _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
+        return t
+
+    def _all_to_all(self, out, inp):
+        if self.world_size == 1:
+            out.copy_(inp)
+            return
+        _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
+
+    def allreduce_scalars(self, sc, slots):
+        """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks."""
+        if self.world_size == 1:
+            return
+        idx = torch.tensor(list(slots), device=sc.device)
+        t = sc.index_select(0, idx)
+        self._allreduce(t)
+        sc.index_copy_(0, idx, t)
+
+    # ------------------------------------------------------------------ shard <-> full layout
+    def _group_rows(self, layout, vec):
+        return {name: t.reshape(t.shape[0], math.prod(t.shape[1:])) for name, t in layout.views(vec).items()}
+
+    def shard(self, full_vec, out=None):
+        """This rank's shard of a full-layout vector."""
+        out = self.zeros() if out is None else out
+        src = self._group_rows(self.full_layout, full_vec)
+        dst = self._group_rows(self.layout, out)
+        for name in GROUPS:
+            if name == "exposure":
+                if self.layout.n_exposure:
+                    dst[name].copy_(src[name])
+                continue
+            dst[name].copy_(src[name][self.lo:self.hi])
+        return out
+
+    def gather_full(self, vec):
+        """The full-layout vector whose shards the ranks hold (all-gather of the Gaussian rows, rank 0's
+        exposure group)."""
+        n, S = self.world_size, self.S
+        names = [g for g in GROUPS if g != "exposure"]
+        rows = self._group_rows(self.layout, vec)
+        widths = [math.prod(self.full_layout.shapes[g][1:]) for g in names]
+        F = sum(widths)
+        pack = torch.zeros(S, F, dtype=vec.dtype, device=vec.device)
+        c = 0
+        for name, w in zip(names, widths):
+            pack[:self.hi - self.lo, c:c + w] = rows[name]
+            c += w
+        allp = torch.empty(n * S, F, dtype=vec.dtype, device=vec.device)
+        if n > 1:
+            _all_gather_into(allp, pack, self.group)
+        else:
+            allp.copy_(pack)
+        out = torch.zeros(self.full_layout.numel, dtype=vec.dtype, device=vec.device)
+        dst = self._group_rows(self.full_layout, out)
+        c = 0
+        for name, w in zip(names, widths):
+            dst[name].copy_(allp[:self.P, c:c + w])
+            c += w
+        e0, e1 = self.full_layout.offsets["exposure"]
+        if self.layout.n_exposure:
+            a0, a1 = self.layout.offsets["exposure"]
+            out[e0:e1] = vec[a0:a1]
+        if n > 1:
+            ex = out[e0:e1].clone()
+            self._allreduce(ex)
+            out[e0:e1] = ex
+        return out
+
+    def zeros(self):
+        return torch.zeros(self.layout.numel, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ LM protocol
+    @property
+    def loss(self):
+        return self.local.loss
+
+    def evaluate(self):
+        loss = self.local.evaluate()
+        self._allreduce(loss)
+        self.local.loss = loss
+        if self.kernel_path:
+            self._exchange_flags()
+        return loss
+
+    def rhs(self, out):
+        full = self.local.rhs(self.local.zeros())
+        self._allreduce(full)
+        return self.shard(full, out)
+
+    def vdot(self, a, b):
+        """<a, b> over the whole vector (host float; the oracle CG of the CPU tests)."""
+        t = (a.double() * b.double()).sum().reshape(1)
+        self._allreduce(t)
+        return float(t)
+
+    def dot(self, a, b, out_slot, damped=False):
+        """This shard's partial of <a, b> [damped] into a device double (cgls_fused all-reduces it)."""
+        from gslm._lib import check, lib
+        bounds, damps = self.layout.group_damp_arrays(self.local.damp) if damped else (None, None)
+        check(lib.gslm_dot(a.data_ptr(), b.data_ptr(), bounds, damps, 7 if damped else 0, a.numel(),
+                           self.local.dot_scratch.data_ptr(), out_slot, self.local.stream), "gslm_dot")
+
+    def damp_add_shard(self, v, y):
+        dv = self._group_rows(self.layout, v)
+        dy = self._group_rows(self.layout, y)
+        damp = self.local.damp
+        for name in GROUPS:
+            d = float(damp[name]) if isinstance(damp, dict) else float(damp)
+            dy[name].add_(dv[name], alpha=d)
+        return y
+
+    def matvec(self, v, y):
+        self.matvec_dot(v, y, None)
+        return y
+
+    def matvec_dot(self, v, y, dot_out, pre=None):
+        if not self.kernel_path:
+            if pre is not None:
+                raise ValueError("the fused direction update needs the HIP operator")
+            vf = self.gather_full(v)
+            yf = self.local.local_normal_matvec(vf, torch.zeros_like(vf), damp=False)
+            self._allreduce(yf)
+            self.shard(yf, y)
+            self.damp_add_shard(v, y)
+            return False
+        return self._matvec_kernels(v, y, dot_out, pre)
+
+    # ------------------------------------------------------------------ HIP path
+    def _buffers(self):
+        if self._bufs is None:
+            n, S, per, dev = self.world_size, self.S, self.per, self.device
+            self._bufs = dict(
+                flags_local=torch.zeros(per, n * S, dtype=torch.int32, device=dev),
+                flags=torch.zeros(per, n * S, dtype=torch.int32, device=dev),
+                trec_send=torch.zeros(per, n * S, 12, dtype=torch.float32, device=dev),
+                trec_recv=torch.zeros(per, n * S, 12, dtype=torch.float32, device=dev),
+                screen_send=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev),
+                screen_recv=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev))
+        return self._bufs
+
+    def _exchange_flags(self):
+        """Once per geometry: visibility / SH-clamp words of this shard's Gaussians in every view."""
+        from gslm._lib import check, lib
+        b = self._buffers()
+        b["flags_local"].zero_()
+        for k, vr in enumerate(self.local.views):
+            check(lib.gslm_view_flags(vr.geom.data_ptr(), self.P, b["flags_local"][k].data_ptr(), self.local.stream),
+                  "gslm_view_flags")
+        for k in range(self.per):
+            self._all_to_all(b["flags"][k], b["flags_local"][k])
+
+    def _pre_opts(self, opts, v, pre):
+        s, num, den = pre[:3]
+        ss = self.layout.grads_struct(s)
+        opts.xpby_s = ctypes.addressof(ss)
+        opts.beta_num, opts.beta_den = num, den
+        e0, e1 = self.layout.offsets["exposure"]
+        if e1 > e0:
+            opts.xpby_tail_v = v.data_ptr() + 4 * e0
+            opts.xpby_tail_s = s.data_ptr() + 4 * e0
+            opts.xpby_tail_n = e1 - e0
+        if len(pre) > 3 and pre[3] is not None:
+            x, anum, aden = pre[3:]
+            opts.alpha_num, opts.alpha_den = anum, aden
+            opts.xpby_x_offset = x.data_ptr() - v.data_ptr()
+        return ss
+
+    def _matvec_kernels(self, v, y, dot_out, pre):
+        from gslm import _lib
+        from gslm._lib import check, lib
+        from gslm.params import raw_gaussians
+        loc = self.local
+        b = self._buffers()
+        n, S, per, P = self.world_size, self.S, self.per, self.P
+        nv = n * per
+        chunk = 16  # views per gslm_tangent_views / gslm_gather_screen call
+        g = raw_gaussians(loc.model)
+        gs = _slice_gaussians(g, self.lo, self.hi)
+        vs = self.layout.grads_struct(v)
+        ys = self.layout.grads_struct(y)
+        vsz = ctypes.sizeof(_lib.GslmView)
+        keep = []
+        if pre is not None and self.hi == self.lo:
+            # empty shard: the direction update has nothing here but rank 0's exposure tail, which an empty
+            # shard never holds (rank 0 owns Gaussians whenever P > 0)
+            pre = None
+        # 1. tangent records of this shard for every view (direction update fused into the first call)
+        for c0 in range(0, nv, chunk):
+            c1 = min(nv, c0 + chunk)
+            opts = None
+            if pre is not None and c0 == 0:
+                opts = _lib.GslmMatvecOpts()
+                keep.append(self._pre_opts(opts, v, pre))
+            vptr = ctypes.cast(ctypes.byref(self.views_kt, c0 * vsz), ctypes.POINTER(_lib.GslmView))
+            check(lib.gslm_tangent_views(vptr, c1 - c0, ctypes.byref(gs), ctypes.byref(vs), int(self.mask_xyz),
+                                         b["flags"].data_ptr() + 4 * c0 * S, S,
+                                         b["trec_send"].data_ptr() + 48 * c0 * S, S,
+                                         None if opts is None else ctypes.byref(opts), loc.stream),
+                  "gslm_tangent_views")
+        # 2. every shard's records of my k-th view
+        for k in range(per):
+            self._all_to_all(b["trec_recv"][k], b["trec_send"][k])
+        # 3. render my views from the exchanged tables: per-Gaussian screen-space sums
+        for k, vr in enumerate(loc.views):
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = 2 | 16  # RENDER | SCREEN
+            opts.flags = 1 if vr.tail_clean else 0  # GSLM_MV_TAIL_CLEAN
+            opts.screen_out = b["screen_send"][k].data_ptr()
+            opts.trec_in = b["trec_recv"][k].data_ptr()
+            check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                          loc.weights[k].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
+                                          vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                          ctypes.byref(vs), ctypes.byref(opts), loc.stream), "gslm_matvec_view_ex")
+            vr.tail_clean = True
+        # 4. my shard's slices of every view's screen sums
+        for k in range(per):
+            self._all_to_all(b["screen_recv"][k], b["screen_send"][k])
+        # 5. every view's chain over my shard, + D v, <v, y>
+        fuse = dot_out is not None and self.hi > self.lo
+        for c0 in range(0, nv, chunk):
+            c1 = min(nv, c0 + chunk)
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = 7 | (8 if c0 == 0 else 0)
+            opts.damp7 = self._damps if c0 == 0 else None
+            opts.screen_stride = S
+            if fuse and c1 == nv:
+                opts.dot_vy = dot_out
+                opts.dot_scratch = loc.dot_scratch.data_ptr()
+                opts.dot_scratch_bytes = loc.dot_scratch.numel() * 8
+            vptr = ctypes.cast(ctypes.byref(self.views_kt, c0 * vsz), ctypes.POINTER(_lib.GslmView))
+            check(lib.gslm_gather_screen(vptr, c1 - c0, ctypes.byref(gs), b["screen_recv"].data_ptr() + 32 * c0 * S,
+                                         ctypes.byref(vs), ctypes.byref(ys), ctypes.byref(opts), loc.stream),
+                  "gslm_gather_screen")
+        e0, e1 = self.layout.offsets["exposure"]
+        if e1 > e0:
+            torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
+        return fuse

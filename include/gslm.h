@@ -240,7 +240,8 @@ int gslm_sh_rest_project(const gslm_view* view, const gslm_gaussians* g, int32_t
 int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const float* screen,
                        const gslm_grads* v, const gslm_grads* y, const gslm_matvec_opts* opts, void* stream);
 
-/* ---- Gaussian-sharded exchange (multi-GPU LM product; gslm.parallel, exchange "gaussian") ----
+/* ---- Gaussian-sharded exchange (multi-GPU LM product; gslm.parallel.GaussianShardedOperator, exchange
+ * "gaussian", the default of gslm.parallel.ShardedLMProblem when every rank renders the same number of views) ----
  * Rank r owns Gaussians [r S, (r + 1) S) of every CG vector and the vector algebra on them.  Per product:
  *   gslm_tangent_views   this shard's tangent render records for EVERY view b (chain_jvp, the TANGENT stage
  *                        of gslm_matvec_view_ex for a Gaussian range) -> all-to-all -> each rank holds its
@@ -257,7 +258,11 @@ int gslm_view_flags(const void* geom, int64_t P, uint32_t* out, void* stream);
  * vflags[b flags_stride + i] is visible (other records untouched), b < nviews (<= 16).  g / v: the shard's
  * leaves and direction (P = shard size, SH-rest stride 3(M-1)); opts (or NULL): only the fused direction
  * update (xpby_s, beta_*, alpha_*, xpby_x_offset, xpby_tail_*) of gslm_matvec_view_ex, applied once before
- * the views' tangents. */
+ * the views' tangents.  The flat tail (xpby_tail_*) is updated once per call, so it must be this rank's
+ * private copy and be passed to one call per product (several calls of one product: only the first gets
+ * opts); an empty shard (P = 0) with a tail still applies the tail's update.
+ * The trec_in table a RENDER stage reads must hold the records of every Gaussian the vflags of that same
+ * geometry (gslm_view_flags of this view's current preprocess) mark visible: the kernel cannot check it. */
 int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const gslm_grads* v,
                        int32_t mask_xyz, const uint32_t* vflags, int64_t flags_stride, float* trec_out,
                        int64_t trec_stride, const gslm_matvec_opts* opts, void* stream);

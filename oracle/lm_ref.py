@@ -130,7 +130,9 @@ class OracleLMProblem:
 
 def cgls_ref(op, g, max_iter, restart_iter, tol=1e-10, atol=0.0):
     """cgls_damped (conjugate_gradient.py:51-127) written on A = J^T J + D in float64 scalars.
-    Same restart schedule and stopping tests as gslm.lm.cgls_fused."""
+    Same restart schedule and stopping tests as gslm.lm.cgls_fused.  An operator whose vectors are shards of
+    the whole (gslm.parallel.GaussianShardedOperator) supplies the global inner product as op.vdot."""
+    vdot = getattr(op, "vdot", None) or (lambda a, b: float((a.double() * b.double()).sum()))
     n = g.numel()
     x = torch.zeros(n, dtype=g.dtype)
     b2 = float(op.loss)
@@ -143,20 +145,20 @@ def cgls_ref(op, g, max_iter, restart_iter, tol=1e-10, atol=0.0):
         else:
             s = g - op.matvec(x, q)
         p = s.clone()
-        gamma = float((s.double() * s.double()).sum())
+        gamma = vdot(s, s)
         stop = False
         for _ in range(restart_iter):
             op.matvec(p, q)
-            delta = float((p.double() * q.double()).sum())
+            delta = vdot(p, q)
             if delta < 1e-20:
                 stop = True
                 break
             alpha = gamma / delta
             x = x + alpha * p
             s = s - alpha * q
-            gamma_new = float((s.double() * s.double()).sum())
+            gamma_new = vdot(s, s)
             p = s + (gamma_new / gamma) * p
-            res = b2 - float((x.double() * g.double()).sum()) - float((x.double() * s.double()).sum())
+            res = b2 - vdot(x, g) - vdot(x, s)
             if res > last_res:
                 stop = True
                 break

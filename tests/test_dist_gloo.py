@@ -43,33 +43,47 @@ def _lm_vector(layout, n):
     return v
 
 
-def _worker(rank, world, port, out_path, ssim=False):
+def _worker(rank, world, port, out_path, ssim=False, exchange="allreduce"):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
-    from gslm.parallel import ShardedOperator, shard_views
+    from gslm.parallel import GaussianShardedOperator, ShardedOperator, shard_views
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     model, cams = _scene()
     mine = [cams[i] for i in shard_views(len(cams), rank, world)]
-    op = ShardedOperator(OracleLMProblem(model, mine, torch.zeros(3), ssim=ssim))
-    loss = op.evaluate()
-    g = op.rhs(op.zeros())
-    v = _lm_vector(op.layout, g.numel())
-    y = op.matvec(v, op.zeros())
-    x = cgls_ref(op, g, 4, 4)
+    local = OracleLMProblem(model, mine, torch.zeros(3), ssim=ssim)
+    if exchange == "gaussian":
+        # CG vectors sharded by Gaussian: the shard layout, shard <-> full maps and the all-reduced CG scalars
+        op = GaussianShardedOperator(local)
+        assert op.layout.P == op.hi - op.lo and op.layout.numel < local.layout.numel
+        loss = op.evaluate()
+        gs = op.rhs(op.zeros())
+        g = op.gather_full(gs)
+        v = _lm_vector(local.layout, g.numel())
+        y = op.gather_full(op.matvec(op.shard(v), op.zeros()))
+        x = op.gather_full(cgls_ref(op, gs, 4, 4))
+    else:
+        op = ShardedOperator(local)
+        loss = op.evaluate()
+        g = op.rhs(op.zeros())
+        v = _lm_vector(op.layout, g.numel())
+        y = op.matvec(v, op.zeros())
+        x = cgls_ref(op, g, 4, 4)
     if rank == 0:
         torch.save({"loss": loss, "g": g, "y": y, "x": x}, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ssim", [False, True])
-def test_sharded_operator_matches_single_process(tmp_path, ssim):
-    """Both residuals: disable_ssim=True ([r; r]) and the SSIM residual ([r1; r2])."""
+@pytest.mark.parametrize("ssim,exchange", [(False, "allreduce"), (True, "allreduce"), (False, "gaussian")])
+def test_sharded_operator_matches_single_process(tmp_path, ssim, exchange):
+    """Both residuals: disable_ssim=True ([r; r]) and the SSIM residual ([r1; r2]); and the
+    Gaussian-sharded vector layout (gslm.parallel.GaussianShardedOperator)."""
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     out = str(tmp_path / "r0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), out, ssim), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, _free_port(), out, ssim, exchange), nprocs=2, start_method="spawn",
+                       join=True)
     got = torch.load(out, weights_only=True)
     model, cams = _scene()
     op = OracleLMProblem(model, cams, torch.zeros(3), ssim=ssim)

@@ -22,12 +22,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _scene():
+def _scene(nv=NV, P=6000):
     from gslm.cameras import orbit_cameras
     from gslm.model import synthetic_gaussians
-    model = synthetic_gaussians(6000, 3, seed=0, s0=0.03, n_cams=NV)
-    gts = [torch.rand(3, H, W, generator=torch.Generator().manual_seed(10 + i)) for i in range(NV)]
-    cams = orbit_cameras(NV, W, H, seed=1, images=gts)
+    model = synthetic_gaussians(P, 3, seed=0, s0=0.03, n_cams=nv)
+    gts = [torch.rand(3, H, W, generator=torch.Generator().manual_seed(10 + i)) for i in range(nv)]
+    cams = orbit_cameras(nv, W, H, seed=1, images=gts)
     return model, cams
 
 
@@ -39,50 +39,81 @@ def _direction(layout, n):
     return v
 
 
-def _run(op, model_layout):
+def _run(op, model_layout, check_every=False):
     from gslm.lm import cgls_fused
     loss = op.evaluate()
     g = op.rhs(op.zeros())
+    if getattr(op, "exchange", None) == "gaussian":  # shard-sized vectors: compare their gathered whole
+        full = op.full_layout
+        v = _direction(full, full.numel).cuda()
+        y = op.gather_full(op.matvec(op.shard(v), op.zeros()))
+        x, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=check_every)
+        res = {"loss": loss.cpu(), "g": op.gather_full(g).cpu(), "y": y.cpu(), "x": op.gather_full(x).cpu()}
+        torch.cuda.synchronize()
+        return res
     v = _direction(model_layout, g.numel()).cuda()
     y = op.matvec(v, op.zeros())
-    x, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=False)
+    x, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=check_every)
     torch.cuda.synchronize()
     return {"loss": loss.cpu(), "g": g.cpu(), "y": y.cpu(), "x": x.cpu()}
 
 
-def _worker(rank, world, port, mode, out_path, ssim=False):
+def _worker(rank, world, port, mode, out_path, ssim=False, nv=NV, P=6000, check_every=False):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gslm.parallel import ShardedLMProblem, shard_views
-    model, cams = _scene()
+    model, cams = _scene(nv, P)
     model = model.to("cuda")
     for c in cams:
         c.to("cuda")
     mine = [cams[i] for i in shard_views(len(cams), rank, world)]
     op = ShardedLMProblem(model, mine, torch.zeros(3), all_cams=cams, exchange=mode, ssim=ssim)
     assert op.exchange == mode
-    res = _run(op, op.layout)
+    res = _run(op, op.layout, check_every)
     if rank == 0:
         torch.save(res, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,ssim", [("screen", False), ("allreduce", False), ("allreduce", True)])
-def test_sharded_gpu_operator_matches_single_process(tmp_path, mode, ssim):
+@pytest.mark.parametrize("mode,ssim,nv,P,check_every", [
+    ("screen", False, NV, 6000, False), ("allreduce", False, NV, 6000, False), ("allreduce", True, NV, 6000, False),
+    # Gaussian-sharded exchange: 2 views per rank, a shard cut inside a 256-Gaussian block
+    ("gaussian", False, 4, 6001, False), ("gaussian", False, NV, 6000, True)])
+def test_sharded_gpu_operator_matches_single_process(tmp_path, mode, ssim, nv, P, check_every):
     from gslm.lm import LMProblem
     out = str(tmp_path / "r0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out, ssim), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out, ssim, nv, P, check_every), nprocs=2,
+                       start_method="spawn", join=True)
     got = torch.load(out, weights_only=True)
-    model, cams = _scene()
+    model, cams = _scene(nv, P)
     model = model.to("cuda")
     for c in cams:
         c.to("cuda")
     op = LMProblem(model, cams, torch.zeros(3), ssim=ssim)
-    ref = _run(op, op.layout)
+    ref = _run(op, op.layout, check_every)
     assert abs(float(got["loss"]) - float(ref["loss"])) <= 1e-9 * float(ref["loss"])
     assert torch.allclose(got["g"], ref["g"], rtol=1e-5, atol=1e-7)
     scale = ref["y"].abs().max()
     assert (got["y"] - ref["y"]).abs().max() <= 1e-5 * scale
+    assert (got["x"] - ref["x"]).norm() <= 1e-4 * ref["x"].norm()
+
+
+def test_gaussian_sharded_single_rank_equals_lmproblem():
+    """world_size 1: the Gaussian-sharded pipeline (tangent_views -> exchanged table -> RENDER | SCREEN ->
+    gather_screen over the one shard) against the fused single-process product, in one process."""
+    from gslm.lm import LMProblem
+    from gslm.parallel import GaussianShardedOperator
+    model, cams = _scene(3, 5000)
+    model = model.to("cuda")
+    for c in cams:
+        c.to("cuda")
+    lp = LMProblem(model, cams, torch.zeros(3))
+    ref = _run(lp, lp.layout)
+    op = GaussianShardedOperator(LMProblem(model, cams, torch.zeros(3)), all_cams=cams)
+    got = _run(op, op.layout)
+    assert abs(float(got["loss"]) - float(ref["loss"])) <= 1e-12 * float(ref["loss"])
+    assert torch.equal(got["g"], ref["g"])
+    assert (got["y"] - ref["y"]).abs().max() <= 1e-5 * ref["y"].abs().max()
     assert (got["x"] - ref["x"]).norm() <= 1e-4 * ref["x"].norm()
