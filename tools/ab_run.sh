@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B timing of library builds with tools/mv_ab.py: bash tools/ab_run.sh <tag> <build_dir>...
+# (build dirs under gaussian-splatting-lm_amd/, e.g. build build_x); then compares the products.
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for L in "$@"; do
+  GSLM_LIB=$PWD/gaussian-splatting-lm_amd/$L/libgslm.so timeout -k 10 240 python tools/mv_ab.py $L --out $OUT \
+    > $OUT/$L.json 2> $OUT/$L.err || { tail -5 $OUT/$L.err; exit 1; }
+  cat $OUT/$L.json
+done
+python tools/mv_ab.py --compare $OUT "$@"

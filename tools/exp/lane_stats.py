@@ -30,7 +30,7 @@ xy, conic, opac = pre["xy"].numpy().astype(np.float32), pre["conic"].numpy().ast
 gx, gy = pre["grid"]
 tiles = range(0, gx * gy, int(sys.argv[1]) if len(sys.argv) > 1 else 41)
 tot = dict(visits=0, lanes=0, valid=0, inv_alpha=0, inv_last=0, inv_outside=0, sub_iters=0, sub_lane_visits=0,
-           pair_iters=0, ent=0, vis_ent=0)
+           pair_iters=0, ent=0, vis_ent=0, half_iters=0)
 for t in tiles:
     s, e = int(rg[t, 0]), int(rg[t, 1])
     if e <= s:
@@ -81,6 +81,13 @@ for t in tiles:
             smax = last[sp].max()
             cnts.append(int((reach[sp].any(axis=0) & (np.arange(n) < smax)).sum()))
         tot["sub_iters"] += max(cnts)
+        # 8x4 halves processed by 32-lane groups
+        cnth = []
+        for hh in range(2):
+            sp = qp.reshape(8, 8)[4 * hh:4 * hh + 4, :].reshape(-1)
+            smax = last[sp].max()
+            cnth.append(int((reach[sp].any(axis=0) & (np.arange(n) < smax)).sum()))
+        tot["half_iters"] += max(cnth)
     # two quadrants per wave (16x8 halves): union visits
     for hq in (0, 1):
         hp = pix[8 * hq:8 * hq + 8, :].reshape(-1)
@@ -92,4 +99,5 @@ print(f"valid lane fraction {tot['valid'] / lanes:.3f}; invalid: alpha region {t
       f"past own n_contrib {tot['inv_last'] / lanes:.3f}, outside image {tot['inv_outside'] / lanes:.3f}")
 print(f"visits per wave (quadrant) schedule {tot['visits']}; 4x4 sub-quadrant groups {tot['sub_iters']} "
       f"({tot['sub_iters'] / tot['visits']:.3f}); 16x8 half-tile waves {tot['pair_iters']} x2 px/lane")
+print(f"8x4 half groups (32 lanes) {tot['half_iters']} ({tot['half_iters'] / tot['visits']:.3f})")
 print(f"visited entries / N_dup {tot['vis_ent'] / tot['ent']:.3f}")
