@@ -184,10 +184,12 @@ int gslm_preprocess(const gslm_view* view, const gslm_gaussians* gi, void* geom,
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
   GeomBufs gb;
   geom_layout(P, const_cast<void*>(geom), &gb);
-  uint32_t h = 0;
-  GSLM_HIP_CHECK(hipMemcpyAsync(&h, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  // a pinned word per host thread: the read-back is one DMA + stream sync instead of a staged pageable copy
+  thread_local uint32_t* pinned = nullptr;
+  if (!pinned) GSLM_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t), hipHostMallocDefault));
+  GSLM_HIP_CHECK(hipMemcpyAsync(pinned, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   GSLM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-  *out = (int64_t)h;
+  *out = (int64_t)*pinned;
   return GSLM_OK;
 }
 

@@ -8,8 +8,7 @@
 //                  2 radix passes over N_dup instead of 6 (SURVEY §7 "Sort"); the sorted values
 //                  ARE the point list.
 //   k_ranges       per-tile [start, end) from key changes (identifyTileRanges).
-//   k_render_fwd   one 16x16 tile per 256-thread block (4 wave64), Gaussian records staged
-//                  through LDS 256 at a time, __syncthreads_count early exit (renderCUDA).
+//   (k_render_fwd, the per-tile blend: render_fwd.hip)
 #include "gslm_internal.hpp"
 #include "gslm_kernels.hpp"
 
@@ -178,94 +177,6 @@ int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int6
   return GSLM_OK;
 }
 
-// renderCUDA forward.  Wave w holds the tile's 8x8 quadrant w (tile_pixel).
-__global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
-                                                     const uint32_t* __restrict__ tile_order,
-                                                     const uint32_t* __restrict__ point_list,
-                                                     const float4* __restrict__ rec, float* __restrict__ out_color,
-                                                     float* __restrict__ out_invdepth, float* __restrict__ final_T,
-                                                     uint32_t* __restrict__ n_contrib) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
-  __shared__ float2 s_r2[TILE_PIX];
-  __shared__ uint64_t s_bits[16];
-  const int tile = (int)tile_order[blockIdx.x];
-  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
-  const int tid = threadIdx.x, w = tid >> 6;
-  int px, py;
-  tile_pixel(tile_x, tile_y, tid, px, py);
-  const bool inside = px < v.W && py < v.H;
-  const float pxf = (float)px, pyf = (float)py;
-  bool done = !inside;
-  const uint2 range = ranges[tile];
-  const int n = (int)(range.y - range.x);
-  const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
-
-  float T = 1.0f;
-  uint32_t last = 0;
-  float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  for (int r = 0; r < rounds; ++r) {
-    const int num_done = __syncthreads_count(done);
-    if (num_done == TILE_PIX) break;
-    const int k = r * TILE_PIX + tid;
-    uint32_t m = 0u;
-    if (k < n) {
-      const uint32_t e = point_list[range.x + k];
-      const int64_t gidx = pl_id(e);
-      m = pl_mask(e);
-      s_r0[tid] = rec[3 * gidx + 0];
-      s_r1[tid] = rec[3 * gidx + 1];
-      const float4 r2 = rec[3 * gidx + 2];
-      s_r2[tid] = make_float2(r2.x, r2.y);
-    }
-    publish_quad_masks(m, s_bits);
-    __syncthreads();
-    // this wave visits, in list order, only the batch elements whose alpha region reaches its quadrant;
-    // software-pipelined: the next hit's records load while this one computes
-    HitIter it(s_bits, w);
-    int j = __ballot(!done) != 0ull ? it.next() : -1;
-    float4 a = s_r0[max(j, 0)], b = s_r1[max(j, 0)];
-    float2 cc = s_r2[max(j, 0)];
-    while (j >= 0) {
-      const int jn = it.next();
-      const float4 an = s_r0[max(jn, 0)], bn = s_r1[max(jn, 0)];
-      const float2 ccn = s_r2[max(jn, 0)];
-      if (!done) {
-        const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-        const float alpha = fminf(0.99f, b.y * gexp(power));
-        if (!(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-          const float test_T = T * (1.0f - alpha);
-          if (test_T < 0.0001f) {
-            done = true;
-          } else {
-            const float wt = alpha * T;
-            C0 += b.z * wt;
-            C1 += b.w * wt;
-            C2 += cc.x * wt;
-            Dp += cc.y * wt;
-            T = test_T;
-            last = (uint32_t)(k - tid + j + 1);  // 1-based list position
-          }
-        }
-      }
-      j = __ballot(!done) != 0ull ? jn : -1;
-      a = an;
-      b = bn;
-      cc = ccn;
-    }
-  }
-  if (inside) {
-    const int64_t pid = (int64_t)py * v.W + px;
-    const int64_t HW = (int64_t)v.H * v.W;
-    final_T[pid] = T;
-    n_contrib[pid] = last;
-    out_color[pid] = C0 + T * v.bg[0];
-    out_color[HW + pid] = C1 + T * v.bg[1];
-    out_color[2 * HW + pid] = C2 + T * v.bg[2];
-    if (out_invdepth) out_invdepth[pid] = Dp;
-  }
-}
-
 // ------------------------------------------------------------------ launchers
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
@@ -320,16 +231,6 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s) {
   if (N <= 0) return GSLM_OK;
   hipLaunchKernelGGL(k_point_ids, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, point_list, out);
-  GSLM_LAUNCH_CHECK();
-  return GSLM_OK;
-}
-
-int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
-                      float* out_invdepth, hipStream_t s) {
-  const int ntiles = v.gx * v.gy;
-  if (ntiles == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_render_fwd, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list, gb.rec,
-                     out_color, out_invdepth, ib.final_T, ib.n_contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -33,7 +33,10 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // ---------------- radix sort (LSD, 8-bit digits, stable) ----------------
 constexpr int SORT_THREADS = 256;
-constexpr int SORT_ITEMS = 16;                       // items per thread per block
+#ifndef GSLM_SORT_ITEMS
+#define GSLM_SORT_ITEMS 16
+#endif
+constexpr int SORT_ITEMS = GSLM_SORT_ITEMS;          // items per thread per block
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS; // 4096 keys per block
 constexpr int RADIX = 256;
 
@@ -47,7 +50,10 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_ITEMS = 8;
+#ifndef GSLM_SCAN_ITEMS
+#define GSLM_SCAN_ITEMS 8
+#endif
+constexpr int SCAN_ITEMS = GSLM_SCAN_ITEMS;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 inline int64_t scan_blocks(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n) * 8 + 64); }  // dual scans: 2 nb
