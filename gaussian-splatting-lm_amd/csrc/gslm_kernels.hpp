@@ -114,17 +114,20 @@ __device__ __forceinline__ QuadCull quad_cull_prep(float gx, float gy, float A, 
 }
 
 // min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of a x^2 + 2 b x y + c y^2
-// (positive definite): 0 if the rectangle holds the centre, else attained on an edge.
+// (positive definite): 0 if the rectangle holds the centre, else attained on an edge that FACES the centre
+// (the segment from any point of the rectangle to the centre, along which the form decreases, leaves the
+// rectangle through such an edge), so at most one vertical and one horizontal edge are evaluated.
 __device__ __forceinline__ double rect_qmin(const QuadCull& q, double x0, double x1, double y0, double y1) {
-  if (x0 <= 0.0 && x1 >= 0.0 && y0 <= 0.0 && y1 >= 0.0) return 0.0;
+  const bool in_x = x0 <= 0.0 && x1 >= 0.0, in_y = y0 <= 0.0 && y1 >= 0.0;
+  if (in_x && in_y) return 0.0;
   double best = INFINITY;
-  const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const double xe = xs[k];
+  if (!in_x) {  // the vertical edge nearer the centre
+    const double xe = x0 > 0.0 ? x0 : x1;
     const double y = fmin(fmax(q.nbc * xe, y0), y1);
-    best = fmin(best, (q.a * xe + 2.0 * q.b * y) * xe + q.c * y * y);
-    const double ye = ys[k];
+    best = (q.a * xe + 2.0 * q.b * y) * xe + q.c * y * y;
+  }
+  if (!in_y) {  // the horizontal edge nearer the centre
+    const double ye = y0 > 0.0 ? y0 : y1;
     const double x = fmin(fmax(q.nba * ye, x0), x1);
     best = fmin(best, (q.c * ye + 2.0 * q.b * x) * ye + q.a * x * x);
   }
