@@ -425,6 +425,57 @@ class LMProblem:
     def damp_add(self, v, y):
         check(lib.gslm_damp_add(v.numel(), v.data_ptr(), self._bounds, self._damps, 7, y.data_ptr(), self.stream))
 
+    # -------------------------------------------------------------- residual-space J and J^T (cgls_residual)
+    def residual_masks(self):
+        """Per view m (.) 1[0 <= R <= 1]: the Jacobian of r = m clamp01(R) - gt w.r.t. the render R."""
+        out = []
+        for b, vr in enumerate(self.views):
+            R = vr.color
+            inside = ((R >= 0) & (R <= 1)).to(torch.float32)
+            m = self.masks[b]
+            out.append(inside if m is None else inside * m.to(torch.float32).reshape(1, vr.H, vr.W))
+        return out
+
+    def jv_residual(self, v, rmasks, out):
+        """out[b] = J_r,b v = m 1[0 <= R <= 1] (.) (d R_b / d theta) v  (the `matvec` of solver_functions.py:83-93,
+        one copy of the [r; r] pair)."""
+        if self.ssim:
+            raise ValueError("jv_residual: the disable_ssim residual only")
+        g = raw_gaussians(self.model)
+        vs = self.layout.grads_struct(v)
+        for b, vr in enumerate(self.views):
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = 1 | 2  # TANGENT | RENDER with jv_out: the colour tangent
+            opts.flags = self.mv_flags
+            opts.jv_out = out[b].data_ptr()
+            check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
+                                          out[b].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N,
+                                          vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
+                                          ctypes.byref(vs), ctypes.byref(opts), self.stream), "gslm_matvec_view_ex(jv)")
+            out[b].mul_(rmasks[b])
+        return out
+
+    def jt_residual(self, r, rmasks, out):
+        """out = J^T [r; r] = 2 sum_b J_r,b^T r_b (the `matvec_T` of solver_functions.py:101-132), xyz and exposure
+        groups zero.  Overwrites out."""
+        g = raw_gaussians(self.model)
+        ys = self.layout.grads_struct(out)
+        for b, vr in enumerate(self.views):
+            seed = (2.0 * rmasks[b]) * r[b]
+            opts = _lib.GslmMatvecOpts()
+            opts.stages = 2 | 4 | (STAGE_OVERWRITE if b == 0 else 0)  # RENDER | GATHER, seeded
+            opts.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
+            opts.pixel_seed = seed.data_ptr()
+            check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(ys), seed.data_ptr(), 1,
+                                          vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
+                                          vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys),
+                                          ctypes.byref(opts), self.stream), "gslm_matvec_view_ex(seed)")
+            vr.tail_clean = True
+        if not self.views:
+            out.zero_()
+        self._apply_mask(out)
+        return out
+
     # -------------------------------------------------------------- device scalar algebra
     def dot(self, a, b, out_slot, damped=False):
         if damped:
@@ -551,6 +602,83 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     return x, {"iters": iter_total, "residuals": history}
 
 
+def cgls_residual(prob, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, verbose=False, callback=None):
+    """cgls_damped (conjugate_gradient.py:51-127) in the reference's own recursion, on the HIP operator: residual-
+    space r (one [3,H,W] image per view standing for the [r; r] pair, so its dots count twice), r -= alpha q with
+    q = J p, a fresh s = J^T r - D x every iteration, and the residual monitor from a fresh J x -- two tangent
+    passes and one seeded adjoint pass per iteration, where cgls_fused runs one fused (J^T J + D) p and updates s
+    algebraically.  Equal iterates in exact arithmetic; this mode keeps long float32 solves on the reference's
+    rounding path.  b = -[r; r] (train_jvp.py:243), x0 = 0.  Returns (x, info)."""
+    if getattr(prob, "ssim", False):
+        raise ValueError("cgls_residual: the disable_ssim residual only")
+    dev = prob.device
+    rm = prob.residual_masks()
+    b = [-r for r in prob.residuals]  # b = -[r; r]: one copy per view
+
+    def dot2(u, v):  # <[u; u], [v; v]> over the views, reduced in float64 on the device (the .item() of :138-146)
+        return 2.0 * sum(float((a.double() * c.double()).sum()) for a, c in zip(u, v))
+
+    n = prob.layout.numel
+    dvec = torch.empty(n, dtype=torch.float64, device=dev)
+    bounds = list(prob._bounds)
+    for k in range(7):
+        dvec[bounds[k]:bounds[k + 1]] = float(prob._damps[k])
+
+    def ddot(u, v):  # dot(x, y, damp) of GaussianModelState (gaussian_model_state.py:262-269)
+        return float((u.double() * v.double() * dvec).sum())
+
+    def Dx(x):
+        return (x.double() * dvec).to(torch.float32)
+
+    jv = [torch.empty_like(t) for t in b]
+    x = torch.zeros(n, dtype=torch.float32, device=dev)
+    s = torch.empty_like(x)
+    iter_total, last_res, history = 0, math.inf, []
+    stop = False
+    while iter_total < max_iter and not stop:
+        prob.jv_residual(x, rm, jv)
+        r = [bb - q for bb, q in zip(b, jv)]                         # r0 = b - A x0
+        prob.jt_residual(r, rm, s)
+        s -= Dx(x)                                                    # s0 = A^T r0 - D x0
+        p = s.clone()
+        gamma = float((s.double() * s.double()).sum())
+        for _ in range(restart_iter):
+            q = [t.clone() for t in prob.jv_residual(p, rm, jv)]      # q = A p
+            delta = dot2(q, q) + ddot(p, p)
+            if delta < 1e-20:
+                if verbose:
+                    print("Early termination: delta is too small.")
+                stop = True
+                break
+            alpha = gamma / delta
+            x += alpha * p
+            r = [rr - alpha * qq for rr, qq in zip(r, q)]
+            prob.jt_residual(r, rm, s)
+            s -= Dx(x)                                                # s = A^T r - D x
+            gamma_prev, gamma = gamma, float((s.double() * s.double()).sum())
+            p = s + (gamma / gamma_prev) * p
+            prob.jv_residual(x, rm, jv)
+            cur = [bb - q for bb, q in zip(b, jv)]                   # cur_r = b - A x
+            res = dot2(cur, cur) + ddot(x, x)
+            history.append(res)
+            if verbose:
+                print(f"[Iter {iter_total + 1}] res: {res:.2e}")
+            if res > last_res:
+                stop = True
+                break
+            last_res = res
+            if callback is not None:
+                callback(x, s, iter_total + 1)
+            if gamma < max(tol * math.sqrt(gamma_prev), atol):
+                stop = True
+                break
+            iter_total += 1
+            if iter_total >= max_iter:
+                stop = True
+                break
+    return x, {"iters": iter_total, "residuals": history}
+
+
 def update_params(model, layout, step, scale):
     """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step."""
     v = layout.views(step)
@@ -565,14 +693,21 @@ def update_params(model, layout, step, scale):
 
 
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
-            verbose=False, device="cuda", sh_projection="auto"):
+            verbose=False, device="cuda", sh_projection="auto", recursion="fused"):
     """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search.
-    With one training view the SH-rest group of the CG vectors is carried projected (LMProblem)."""
+    With one training view the SH-rest group of the CG vectors is carried projected (LMProblem).
+    recursion: "fused" (cgls_fused, one fused (J^T J + D) p per iteration) or "cgls" (cgls_residual, the
+    reference's residual-space recursion)."""
     prob = LMProblem(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device, sh_projection=sh_projection)
     start_loss = prob.evaluate()
-    g = prob.rhs(prob.zeros())
-    s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
-                         verbose=verbose)
+    if recursion == "cgls":
+        s, info = cgls_residual(prob, max_iter=max_iter, restart_iter=restart_iter, verbose=verbose)
+    elif recursion == "fused":
+        g = prob.rhs(prob.zeros())
+        s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
+                             verbose=verbose)
+    else:
+        raise ValueError(f"recursion must be 'fused' or 'cgls', got {recursion!r}")
     s = prob.expand(s)
     del prob
     val = LMProblem(model, val_cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)

@@ -252,3 +252,49 @@ def test_culled_gaussians_get_exact_zero_rows():
         views = prob.layout.views(g)
         for name in ("features_dc", "features_rest", "scaling", "rotation", "opacity"):
             assert float(views[name][culled].abs().max()) == 0.0, name
+
+
+@pytest.mark.parametrize("sched,key,tol", [((2, 1), "x_ref_schedule", 1e-5), ((10, 10), "x_ten", 1e-4)])
+def test_cgls_residual_matches_reference_schedule(sched, key, tol):
+    """The reference's own recursion (conjugate_gradient.py:93-104: r -= alpha q, fresh J^T r - D x, fresh
+    residual monitor) on the HIP operator against the reference solver's iterates."""
+    from gslm.lm import LMProblem, cgls_residual
+    d, m, cams = _load()
+    prob = LMProblem(m, cams, torch.zeros(3))
+    prob.evaluate()
+    x, info = cgls_residual(prob, max_iter=sched[0], restart_iter=sched[1])
+    ref = d[key]
+    err = np.linalg.norm(x.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref)
+    assert err < tol, err
+
+
+def test_recursions_against_float64_oracle():
+    """10 CGLS iterations of the two float32 recursions (fused normal-equation, residual-space) against the float64
+    oracle's CGLS on the golden scene: both stay within 1e-4 of it, and of each other (DESIGN.md reports the
+    drift)."""
+    import copy
+    from gslm.lm import LMProblem, cgls_fused, cgls_residual
+    from oracle.lm_ref import OracleLMProblem, cgls_ref
+    d, m, cams = _load()
+    mc = copy.deepcopy(m).to("cpu")
+    for t in mc.params():
+        t.data = t.data.double()
+    ccs = []
+    for c in cams:
+        cc = copy.deepcopy(c).to("cpu")
+        for k in ("original_image", "alpha_mask", "world_view_transform", "projection_matrix", "full_proj_transform",
+                  "camera_center"):
+            setattr(cc, k, getattr(cc, k).double())
+        ccs.append(cc)
+    op = OracleLMProblem(mc, ccs, torch.zeros(3, dtype=torch.float64))
+    op.evaluate()
+    x64 = cgls_ref(op, op.rhs(), 10, 10)
+    prob = LMProblem(m, cams, torch.zeros(3))
+    prob.evaluate()
+    xf, _ = cgls_fused(prob, prob.rhs(prob.zeros()), max_iter=10, restart_iter=10, check_every=True)
+    xr, _ = cgls_residual(prob, max_iter=10, restart_iter=10)
+    ef = float((xf.double().cpu() - x64).norm() / x64.norm())
+    er = float((xr.double().cpu() - x64).norm() / x64.norm())
+    efr = float((xf.double() - xr.double()).norm().cpu() / x64.norm())
+    print(f"10-iteration drift vs float64 oracle: fused {ef:.3e}, residual-space {er:.3e}, between {efr:.3e}")
+    assert ef < 1e-4 and er < 1e-4 and efr < 1e-4, (ef, er, efr)
