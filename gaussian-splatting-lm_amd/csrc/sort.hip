@@ -75,84 +75,84 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
   if (tid == 0) totals[d] = carry;
 }
 
-// Scatter of one pass: the block ranks its 4096 keys by digit (stable: round, then wave, then lane order),
-// reorders them through LDS into digit-sorted order, and writes each digit's run to its global offset
-// from consecutive threads -- coalesced segments instead of one scattered 4-byte store per key.
+// Scatter of one pass.  Each wave ranks a contiguous quarter of the block's 4096 keys on its own (16 rounds of
+// 64 consecutive keys): a digit "match" from nbits wave ballots gives the key's rank among equal digits of the
+// round, and a wave-private LDS counter per digit carries the wave's running count across rounds (LDS accesses
+// of one wave are ordered, so no barrier inside the loop).  One block-wide prefix then turns the four waves'
+// counts into local positions: block order = wave order, round order, lane order = input order (stable).  The
+// keys are reordered through LDS into digit runs and each run is written to its global offset by consecutive
+// threads (coalesced segments instead of one scattered 4-byte store per key).
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout, int64_t n, int shift, const uint32_t* __restrict__ hist, int nblocks,
+    uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
     const uint32_t* __restrict__ totals) {
+  static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
+  constexpr int WAVE_KEYS = SORT_TILE / 4;
   __shared__ uint32_t s_keys[SORT_TILE], s_vals[SORT_TILE];
-  __shared__ uint32_t s_run[RADIX];    // running per-digit count in this block, then the digit's local start
-  __shared__ uint32_t s_gbase[RADIX];  // global offset of this block's run of each digit
-  __shared__ uint32_t s_wc[4][RADIX];
+  __shared__ uint32_t s_wcnt[4][RADIX];  // per-wave running digit count, then the wave's offset in the digit run
+  __shared__ uint32_t s_loc[RADIX];      // block-local start of each digit's run
+  __shared__ uint32_t s_gbase[RADIX];    // global offset of this block's run of each digit
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
   const int nvalid = (int)min<int64_t>(SORT_TILE, n - base);
+  const int wbase = w * WAVE_KEYS;
 
-  // issue all loads first (16 keys + 16 values per thread in flight)
-  uint32_t key[SORT_ITEMS], val[SORT_ITEMS], lidx[SORT_ITEMS];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s_wcnt[w][lane + 64 * k] = 0u;
+  // all loads first (16 keys + 16 values per lane in flight), wave w on keys [wbase, wbase + 1024) of the block
+  uint32_t key[SORT_ITEMS], val[SORT_ITEMS], lrank[SORT_ITEMS];
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
-    const int64_t i = base + r * SORT_THREADS + tid;
+    const int64_t i = base + wbase + r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
     val[r] = i < n ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == NULL: the values are the indices
   }
   {
-    // digit base for this block = exclusive prefix of digit totals + this block's offset
+    // global base of each digit's run for this block = exclusive prefix of digit totals + this block's offset
     const uint32_t t = totals[tid];
     uint32_t tot;
     const uint32_t inc = block_incl_scan256(t, s_w, &tot);
     s_gbase[tid] = inc - t + hist[(int64_t)tid * nblocks + blockIdx.x];
-    s_run[tid] = 0u;
   }
-  __syncthreads();
-
-  // 1. local rank of every key within its digit (elements of one round: wave order, then lane order)
+  // 1. wave-local stable rank of every key among equal digits
   const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
-    const bool valid = r * SORT_THREADS + tid < nvalid;
+    const bool valid = wbase + r * 64 + lane < nvalid;
     const uint32_t d = (key[r] >> shift) & (RADIX - 1);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s_wc[w][lane + 64 * k] = 0u;
     unsigned long long m = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
+      if (b >= nbits) break;
       const bool bit = (d >> b) & 1u;
       const unsigned long long bb = __ballot(bit);
       m &= bit ? bb : ~bb;
     }
     const uint32_t rank = __popcll(m & lt_mask);
-    if (valid && rank == 0) s_wc[w][d] = (uint32_t)__popcll(m);
-    __syncthreads();
-    {
-      const uint32_t c0 = s_wc[0][tid], c1 = s_wc[1][tid], c2 = s_wc[2][tid], c3 = s_wc[3][tid];
-      const uint32_t b0 = s_run[tid];
-      s_wc[0][tid] = b0;
-      s_wc[1][tid] = b0 + c0;
-      s_wc[2][tid] = b0 + c0 + c1;
-      s_wc[3][tid] = b0 + c0 + c1 + c2;
-      s_run[tid] = b0 + c0 + c1 + c2 + c3;
-    }
-    __syncthreads();
-    lidx[r] = s_wc[w][d] + rank;
-    __syncthreads();
+    const uint32_t cnt = s_wcnt[w][d];
+    lrank[r] = cnt + rank;
+    if (valid && rank == 0) s_wcnt[w][d] = cnt + (uint32_t)__popcll(m);
   }
-  // 2. digit-sorted order in LDS: local start of each digit = exclusive prefix of the block's counts
+  __syncthreads();
+  // 2. the four waves' offsets inside each digit's run, and each run's block-local start
   {
-    const uint32_t c = s_run[tid];
+    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
+    const uint32_t c = c0 + c1 + c2 + c3;
+    s_wcnt[0][tid] = 0u;
+    s_wcnt[1][tid] = c0;
+    s_wcnt[2][tid] = c0 + c1;
+    s_wcnt[3][tid] = c0 + c1 + c2;
     uint32_t tot;
     const uint32_t inc = block_incl_scan256(c, s_w, &tot);
-    s_run[tid] = inc - c;
+    s_loc[tid] = inc - c;
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
-    if (r * SORT_THREADS + tid < nvalid) {
+    if (wbase + r * 64 + lane < nvalid) {
       const uint32_t d = (key[r] >> shift) & (RADIX - 1);
-      const uint32_t lp = s_run[d] + lidx[r];
+      const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
       s_keys[lp] = key[r];
       s_vals[lp] = val[r];
     }
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   for (int e = tid; e < nvalid; e += SORT_THREADS) {
     const uint32_t k = s_keys[e];
     const uint32_t d = (k >> shift) & (RADIX - 1);
-    const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_run[d]);
+    const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_loc[d]);
     kout[pos] = k;
     vout[pos] = s_vals[e];
   }
@@ -335,8 +335,10 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
   for (int shift = 0; shift < end_bit; shift += 8) {
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+    const int nbits = end_bit - shift < 8 ? end_bit - shift : 8;  // digit bits of this pass (the last may be short)
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki,
-                       (first && iota_values) ? (const uint32_t*)nullptr : vi, ko, vo, n, shift, hist, nb, totals);
+                       (first && iota_values) ? (const uint32_t*)nullptr : vi, ko, vo, n, shift, nbits, hist, nb,
+                       totals);
     first = false;
     GSLM_LAUNCH_CHECK();
     std::swap(ki, ko);
