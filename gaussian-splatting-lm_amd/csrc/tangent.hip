@@ -10,53 +10,81 @@
 
 namespace gslm {
 
-// p = s + beta p over this block's 256 Gaussians' slices of every group (coalesced, 8 loads in flight
-// per thread), and the flat tail by block 0.  Same arithmetic as k_xpby_dev (bitwise).
+// p = s + beta p over this block's 256 Gaussians' slices of every group, and the flat tail by block 0.
+// Same arithmetic as k_xpby_dev (bitwise).  The narrow groups (xyz, dc, scaling, rotation, opacity, and the
+// SH rest when projected: <= 4 floats per Gaussian, so <= 4 elements per thread each) are loaded in one pass --
+// every s / p / x load of the block in flight before the first store -- instead of one latency per group; a
+// full-layout SH rest (3(M-1) floats per Gaussian) streams in its own loop.
 __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_rest) {
   const float b = (float)((*xp.num) / (*xp.den));
   const bool with_x = xp.anum != nullptr;
   const float a = with_x ? (float)((*xp.anum) / (*xp.aden)) : 0.f;  // gslm_cg_update's alpha, bitwise
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t nv = min((int64_t)blockDim.x, P - i0);
-  constexpr int U = 8;
+  const int tid = threadIdx.x;
+  constexpr int MAXW[6] = {3, 3, 3, 3, 4, 1};  // per-Gaussian widths the one-pass path covers
+  const bool rest_narrow = xp.w[2] <= 3;
+  float sv[17], pv[17], xv[17];
+  int n = 0;
+#pragma unroll
   for (int k = 0; k < 6; ++k) {
-    if (!xp.p[k]) continue;
-    float* p = xp.p[k] + i0 * xp.w[k];
-    const float* s = xp.s[k] + i0 * xp.w[k];
-    const int64_t len = nv * xp.w[k];
+#pragma unroll
+    for (int j = 0; j < MAXW[k]; ++j, ++n) {
+      const int64_t e = (int64_t)j * blockDim.x + tid;
+      const bool on = xp.p[k] && (k != 2 || rest_narrow) && e < nv * xp.w[k];
+      const int64_t gi = i0 * xp.w[k] + e;
+      sv[n] = on ? xp.s[k][gi] : 0.f;
+      pv[n] = on ? xp.p[k][gi] : 0.f;
+      xv[n] = (on && with_x) ? xp.p[k][xp.xoff + gi] : 0.f;
+    }
+  }
+  n = 0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+#pragma unroll
+    for (int j = 0; j < MAXW[k]; ++j, ++n) {
+      const int64_t e = (int64_t)j * blockDim.x + tid;
+      const bool on = xp.p[k] && (k != 2 || rest_narrow) && e < nv * xp.w[k];
+      if (on) {
+        const int64_t gi = i0 * xp.w[k] + e;
+        if (with_x) xp.p[k][xp.xoff + gi] = xv[n] + a * pv[n];
+        const float r = sv[n] + b * pv[n];
+        xp.p[k][gi] = r;
+        if (k == 2) s_rest[e] = r;  // the SH-rest slice stays in LDS for the tangent below
+      }
+    }
+  }
+  if (xp.p[2] && !rest_narrow) {
+    float* p = xp.p[2] + i0 * xp.w[2];
+    const float* s = xp.s[2] + i0 * xp.w[2];
+    const int64_t len = nv * xp.w[2];
+    constexpr int U = 8;
     for (int64_t e0 = 0; e0 < len; e0 += (int64_t)U * blockDim.x) {
-      float sv[U], pv[U];
+      float su[U], pu[U], xu[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
-        sv[u] = e < len ? s[e] : 0.f;
-        pv[u] = e < len ? p[e] : 0.f;
-      }
-      float xv[U];
-      if (with_x) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
-          xv[u] = e < len ? p[xp.xoff + e] : 0.f;
-        }
+        const int64_t e = e0 + (int64_t)u * blockDim.x + tid;
+        su[u] = e < len ? s[e] : 0.f;
+        pu[u] = e < len ? p[e] : 0.f;
+        xu[u] = (e < len && with_x) ? p[xp.xoff + e] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t e = e0 + (int64_t)u * blockDim.x + threadIdx.x;
+        const int64_t e = e0 + (int64_t)u * blockDim.x + tid;
         if (e < len) {
-          if (with_x) p[xp.xoff + e] = xv[u] + a * pv[u];
-          const float r = sv[u] + b * pv[u];
+          if (with_x) p[xp.xoff + e] = xu[u] + a * pu[u];
+          const float r = su[u] + b * pu[u];
           p[e] = r;
-          if (k == 2) s_rest[e] = r;  // the SH-rest slice stays in LDS for the tangent below
+          s_rest[e] = r;
         }
       }
     }
   }
   if (blockIdx.x == 0 && xp.tail_p)
     for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) {
-      const float pv = xp.tail_p[e];
-      if (with_x) xp.tail_p[xp.xoff + e] = xp.tail_p[xp.xoff + e] + a * pv;
-      xp.tail_p[e] = xp.tail_s[e] + b * pv;
+      const float pvt = xp.tail_p[e];
+      if (with_x) xp.tail_p[xp.xoff + e] = xp.tail_p[xp.xoff + e] + a * pvt;
+      xp.tail_p[e] = xp.tail_s[e] + b * pvt;
     }
 }
 
