@@ -66,8 +66,15 @@ struct PreOut {
 // (A, B, C) the stored conic.  The float evaluation of Q in the tile passes (-ffp-contract=off, a
 // handful of roundings per term, |2 B dx dy| <= max(A, C) |d|^2) errs by at most 14 eps (A + C) |d|^2,
 // so every pixel a pass can accept satisfies d^T (Q - e I) d <= t with e = 32 eps (A + C).  The
-// quadrant test evaluates min over the quadrant of d^T (Q - e I) d in double and compares with
-// tq = t * 1.02 + 1e-4 (exp / log / 1/255-constant rounding), rounded up to float.
+// quadrant test bounds min over the quadrant of d^T (Q - e I) d from below and rejects the quadrant only
+// when that bound exceeds tq = t * 1.02 + 1e-4 (exp / log / 1/255-constant rounding), rounded up to float.
+//
+// The minimisation runs in float (k_duplicate evaluates it for every (tile, Gaussian) pair: in double it
+// cost 46 of the kernel's 80 us at 1M Gaussians / 1080p).  Its value at the chosen point is lowered by a
+// rounding bound before the comparison: 2e-6 of the terms' magnitude (a few float roundings of a
+// 5-term expression, 8x over), the gradient times the rounding of the pixel offsets (tile origin minus
+// centre: <= 4e-7 (|gx| + |gy| + 8192)), and 1e-5 absolute (the edge minimiser's rounding is second
+// order).  Looser than exact only ever keeps a quadrant, so the cull stays exact.
 
 // tq for effective opacity o; negative when o <= 1/255 (no pixel can ever pass).
 __device__ __forceinline__ float alpha_threshold(float op_eff) {
@@ -81,7 +88,7 @@ __device__ __forceinline__ float alpha_threshold(float op_eff) {
 // Per-Gaussian part of the quadrant test (k_duplicate prepares it once and tests every tile of the
 // rect).  mode: 0 = reaches no pixel, 1 = treat every quadrant as reachable, 2 = test.
 struct QuadCull {
-  double gx, gy, a, b, c, nba, nbc, tq;
+  float gx, gy, a, b, c, nba, nbc, tq, dpos;
   int mode;
 };
 
@@ -97,39 +104,49 @@ __device__ __forceinline__ QuadCull quad_cull_prep(float gx, float gy, float A, 
     q.mode = 0;
     return q;
   }
-  const double e = 32.0 * 5.9604644775390625e-8 * ((double)A + (double)C);
-  q.a = (double)A - e;
-  q.c = (double)C - e;
-  q.b = (double)B;
-  if (!(q.a > 0.0 && q.c > 0.0 && q.a * q.c - q.b * q.b > 0.0)) {  // unbounded (or NaN) region
+  const float e = 32.0f * 5.9604644775390625e-8f * (A + C);
+  q.a = A - e;
+  q.c = C - e;
+  q.b = B;
+  // unbounded, nearly degenerate (the float minimiser would be ill-conditioned) or NaN: every quadrant
+  if (!(q.a > 0.0f && q.c > 0.0f && q.a * q.c - q.b * q.b > 1e-6f * (q.a * q.c))) {
     q.mode = 1;
     return q;
   }
   q.nba = -q.b / q.a;  // edge minimisers; their rounding changes the edge minimum only to second order
   q.nbc = -q.b / q.c;
-  q.gx = (double)gx;
-  q.gy = (double)gy;
-  q.tq = (double)tq;
+  q.gx = gx;
+  q.gy = gy;
+  q.tq = tq;
+  q.dpos = 4e-7f * (fabsf(gx) + fabsf(gy) + 8192.0f);
   return q;
 }
 
-// min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of a x^2 + 2 b x y + c y^2
-// (positive definite): 0 if the rectangle holds the centre, else attained on an edge that FACES the centre
-// (the segment from any point of the rectangle to the centre, along which the form decreases, leaves the
-// rectangle through such an edge), so at most one vertical and one horizontal edge are evaluated.
-__device__ __forceinline__ double rect_qmin(const QuadCull& q, double x0, double x1, double y0, double y1) {
-  const bool in_x = x0 <= 0.0 && x1 >= 0.0, in_y = y0 <= 0.0 && y1 >= 0.0;
-  if (in_x && in_y) return 0.0;
-  double best = INFINITY;
+// Q at the offset (x, y) minus its rounding bound (see above).
+__device__ __forceinline__ float q_lower(const QuadCull& q, float x, float y) {
+  const float ax = q.a * x, by = q.b * y, bx = q.b * x, cy = q.c * y;
+  const float val = (ax + 2.0f * by) * x + cy * y;
+  const float mag = (fabsf(ax) + 2.0f * fabsf(by)) * fabsf(x) + fabsf(cy * y);
+  const float grad = 2.0f * (fabsf(ax) + fabsf(by) + fabsf(bx) + fabsf(cy));
+  return val - (2e-6f * mag + grad * q.dpos + 1e-5f);
+}
+
+// Lower bound of min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of
+// a x^2 + 2 b x y + c y^2 (positive definite): 0 if the rectangle holds the centre, else the minimum is on an
+// edge that FACES the centre (the segment from any point of the rectangle to the centre, along which the form
+// decreases, leaves the rectangle through such an edge), so at most one vertical and one horizontal edge are
+// evaluated.
+__device__ __forceinline__ float rect_qmin(const QuadCull& q, float x0, float x1, float y0, float y1) {
+  const bool in_x = x0 <= 0.0f && x1 >= 0.0f, in_y = y0 <= 0.0f && y1 >= 0.0f;
+  if (in_x && in_y) return 0.0f;
+  float best = INFINITY;
   if (!in_x) {  // the vertical edge nearer the centre
-    const double xe = x0 > 0.0 ? x0 : x1;
-    const double y = fmin(fmax(q.nbc * xe, y0), y1);
-    best = (q.a * xe + 2.0 * q.b * y) * xe + q.c * y * y;
+    const float xe = x0 > 0.0f ? x0 : x1;
+    best = q_lower(q, xe, fminf(fmaxf(q.nbc * xe, y0), y1));
   }
   if (!in_y) {  // the horizontal edge nearer the centre
-    const double ye = y0 > 0.0 ? y0 : y1;
-    const double x = fmin(fmax(q.nba * ye, x0), x1);
-    best = fmin(best, (q.c * ye + 2.0 * q.b * x) * ye + q.a * x * x);
+    const float ye = y0 > 0.0f ? y0 : y1;
+    best = fminf(best, q_lower(q, fminf(fmaxf(q.nba * ye, x0), x1), ye));
   }
   return best;
 }
@@ -138,12 +155,12 @@ __device__ __forceinline__ double rect_qmin(const QuadCull& q, double x0, double
 // quadrant s = pixels [8 (s & 1), +7] x [8 (s >> 1), +7] of the tile (wave s).
 __device__ __forceinline__ uint32_t quad_mask(const QuadCull& q, int tile_x, int tile_y) {
   if (q.mode != 2) return q.mode ? 0xFu : 0u;
-  const double bx = (double)(tile_x * TILE_X) - q.gx, by = (double)(tile_y * TILE_Y) - q.gy;
+  const float bx = (float)(tile_x * TILE_X) - q.gx, by = (float)(tile_y * TILE_Y) - q.gy;
   uint32_t m = 0u;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const double x0 = bx + 8.0 * (s & 1), y0 = by + 8.0 * (s >> 1);
-    if (!(rect_qmin(q, x0, x0 + 7.0, y0, y0 + 7.0) > q.tq)) m |= 1u << s;
+    const float x0 = bx + 8.0f * (float)(s & 1), y0 = by + 8.0f * (float)(s >> 1);
+    if (!(rect_qmin(q, x0, x0 + 7.0f, y0, y0 + 7.0f) > q.tq)) m |= 1u << s;
   }
   return m;
 }
