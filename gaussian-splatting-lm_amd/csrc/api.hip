@@ -53,6 +53,7 @@ size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
   b.hist = c.take<uint32_t>(sort_hist_bytes(N) / 4);
   b.ranges = c.take<uint2>(ntiles);
   b.tile_order = c.take<uint32_t>(ntiles);
+  b.tile_neff = c.take<uint32_t>(ntiles);
   b.end_bit = 1;
   while ((1ll << b.end_bit) < (long long)ntiles) ++b.end_bit;
   b.passes = (b.end_bit + 7) / 8;
@@ -77,6 +78,8 @@ size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* o) {
   ScratchBufs b;
   b.trec = c.take<float4>((size_t)P * REC_F4);
   b.contrib = c.take<float4>((size_t)N * REC_F4);
+  b.hscan = c.take<uint32_t>((size_t)N + 1);
+  b.scan_tmp = c.take<uint32_t>(scan_tmp_bytes(N) / 4);
   if (o) *o = b;
   return c.off;
 }

@@ -79,13 +79,13 @@ int launch_render_vjp_lm(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, 
                          const float* dL_dcolor, const ScratchBufs& sb, bool tail_clean, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (N == 0) return GSLM_OK;
-  if (!tail_clean) {  // slots and tail rows: once per geometry, shared with k_render_matvec
-    const int st = launch_row_slots(v, gb, bb, N, s);
+  if (!tail_clean) {  // the LM row map: once per geometry, shared with k_render_matvec
+    const int st = launch_lm_rowmap(v, gb, bb, ib, sb, N, s);
     if (st) return st;
   }
   hipLaunchKernelGGL((k_render_bwd<false, false, 2>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                      bb.point_list, gb.rec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, nullptr,
-                     sb.contrib, tail_clean ? 0 : 1);
+                     sb.contrib, 0);  // head rows only (launch_lm_rowmap)
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -18,6 +18,7 @@ namespace gslm {
 __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* __restrict__ rec,
                                                         const uint32_t* __restrict__ tiles,
                                                         const uint32_t* __restrict__ goff,
+                                                        const uint32_t* __restrict__ hscan,
                                                         const float4* __restrict__ rows, float4* __restrict__ out) {
   __shared__ float4 s_buf[GATHER_CHUNK * 2];
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
@@ -25,9 +26,11 @@ __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* 
   const int64_t nvalid = min((int64_t)blockDim.x, P - i0);
   const uint32_t n = i < P ? tiles[i] : 0u;
   float G2[NV];
+  // the Gaussian's head rows of the LM row map (k_gather_lm)
   const int64_t il = i0 + nvalid - 1;
-  const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
-  block_sum_rows<2>(rows, R0, R1, i < P ? goff[i] : R1, n, s_buf, G2);
+  const uint32_t R0 = hscan[goff[i0]], R1 = hscan[goff[il] + tiles[il]];
+  const uint32_t h0 = i < P ? hscan[goff[i]] : R1, h1 = i < P ? hscan[goff[i] + n] : R1;
+  block_sum_rows<2>(rows, R0, R1, h0, h1 - h0, s_buf, G2);
   if (i >= P) return;
   const uint32_t flags = n ? (0x80000000u | (__float_as_uint(rec[3 * i + 2].z) & 7u)) : 0u;
   out[2 * i + 0] = make_float4(G2[2], G2[3], G2[4], G2[5]);
@@ -76,7 +79,7 @@ __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, cons
 int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   hipLaunchKernelGGL(k_rowsum_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, g.P, gb.rec, gb.tiles,
-                     gb.goff, sb.contrib, reinterpret_cast<float4*>(out));
+                     gb.goff, sb.hscan, sb.contrib, reinterpret_cast<float4*>(out));
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

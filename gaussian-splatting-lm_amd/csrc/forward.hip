@@ -169,6 +169,63 @@ __global__ __launch_bounds__(256) void k_row_slots(int64_t N, int gx, const uint
   slots[k] = row_slot(goff[g], rect[g], (int)(t % (uint32_t)gx), (int)(t / (uint32_t)gx));
 }
 
+// ---- the LM row map (ScratchBufs::hscan), once per geometry ----
+// largest n_contrib over each tile's pixels: list positions at or past it are blended by no pixel of the tile
+__global__ __launch_bounds__(256) void k_tile_neff(ViewK v, const uint32_t* __restrict__ n_contrib,
+                                                    uint32_t* __restrict__ neff) {
+  __shared__ int s_w[4];
+  const int tile = blockIdx.x, tile_x = tile % v.gx, tile_y = tile / v.gx;
+  int px, py;
+  tile_pixel(tile_x, tile_y, threadIdx.x, px, py);
+  int wm = (px < v.W && py < v.H) ? (int)n_contrib[(int64_t)py * v.W + px] : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) wm = max(wm, __shfl_xor(wm, o));
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = wm;
+  __syncthreads();
+  if (threadIdx.x == 0) neff[tile] = (uint32_t)max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+}
+
+// head flag of every sorted entry at its goff-order slot, and the goff slot itself in slots[k]
+__global__ __launch_bounds__(256) void k_row_flags(int64_t N, int gx, const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ point_list,
+                                                    const uint2* __restrict__ ranges, const uint32_t* __restrict__ neff,
+                                                    const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
+                                                    uint32_t* __restrict__ slots, uint32_t* __restrict__ flags) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const uint32_t t = keys[k];
+  const uint32_t g = pl_id(point_list[k]);
+  const uint32_t o = row_slot(goff[g], rect[g], (int)(t % (uint32_t)gx), (int)(t / (uint32_t)gx));
+  slots[k] = o;
+  flags[o] = ((uint32_t)k - ranges[t].x) < neff[t] ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_row_final(int64_t N, const uint32_t* __restrict__ hscan,
+                                                    uint32_t* __restrict__ slots) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < N) slots[k] = hscan[slots[k]];  // tails get the next head's slot; they are never written
+}
+
+int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,
+                     int64_t N, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (N <= 0 || ntiles == 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(sb.hscan, 0, sizeof(uint32_t), s));
+    return GSLM_OK;
+  }
+  const unsigned nb = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_tile_neff, dim3(ntiles), dim3(TILE_PIX), 0, s, v, ib.n_contrib, bb.tile_neff);
+  hipLaunchKernelGGL(k_row_flags, dim3(nb), dim3(256), 0, s, N, v.gx, bb.keys_sorted, bb.point_list, bb.ranges,
+                     bb.tile_neff, gb.goff, gb.rect, bb.slots, sb.hscan);
+  GSLM_LAUNCH_CHECK();
+  // in place: every thread reads its elements before writing them
+  const int st = exclusive_scan_u32(sb.hscan, nullptr, sb.hscan, N, sb.scan_tmp, sb.hscan + N, s);
+  if (st) return st;
+  hipLaunchKernelGGL(k_row_final, dim3(nb), dim3(256), 0, s, N, sb.hscan, bb.slots);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s) {
   if (N <= 0) return GSLM_OK;
   hipLaunchKernelGGL(k_row_slots, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, v.gx, bb.keys_sorted,

@@ -85,6 +85,7 @@ template <bool WANT_MEANS, int ROWF4>
 __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
+                                                    const uint32_t* __restrict__ hscan,
                                                     const float4* __restrict__ rows, FlatK o) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // row chunks, then the factored SH stage
   __shared__ double s_dot[4];
@@ -95,9 +96,11 @@ __global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const floa
   const uint32_t n = i < g.P ? tiles[i] : 0u;
   float G2[NV];
   {
+    // this Gaussian's head rows (the LM row map): [hscan[goff], hscan[goff + tiles])
     const int64_t il = i0 + nvalid - 1;
-    const uint32_t R0 = goff[i0], R1 = goff[il] + tiles[il];
-    block_sum_rows<ROWF4>(rows, R0, R1, i < g.P ? goff[i] : R1, n, reinterpret_cast<float4*>(s_rest), G2);
+    const uint32_t R0 = hscan[goff[i0]], R1 = hscan[goff[il] + tiles[il]];
+    const uint32_t h0 = i < g.P ? hscan[goff[i]] : R1, h1 = i < g.P ? hscan[goff[i] + n] : R1;
+    block_sum_rows<ROWF4>(rows, R0, R1, h0, h1 - h0, reinterpret_cast<float4*>(s_rest), G2);
   }
   ChainOut co;
   if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, WANT_MEANS, co);
@@ -200,10 +203,10 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
   const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
   if (mask_xyz)
     hipLaunchKernelGGL((k_gather_lm<false, 2>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
-                       sb.contrib, o);
+                       sb.hscan, sb.contrib, o);
   else
     hipLaunchKernelGGL((k_gather_lm<true, 3>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
-                       sb.contrib, o);
+                       sb.hscan, sb.contrib, o);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -336,9 +336,10 @@ struct BinBufs {
   uint32_t* hist;
   uint2* ranges;
   uint32_t* tile_order;   // tiles by descending list length: the launch order of the tile passes
-  uint32_t* slots;        // [N] gradient-row slot of each sorted entry (row_slot, k_row_slots), in the
-                          // sort's free ping-pong key buffer; valid only once the fused LM product
-                          // computed it for the current binning
+  uint32_t* slots;        // [N] gradient-row slot of each sorted entry, in the sort's free ping-pong key
+                          // buffer: the LM row map (launch_lm_rowmap) once an LM product computed it for the
+                          // current binning
+  uint32_t* tile_neff;    // [ntiles] largest n_contrib of each tile's pixels (the LM row map's head bound)
   int passes;
   int end_bit;
 };
@@ -355,6 +356,12 @@ struct ImgBufs {
 struct ScratchBufs {
   float4* trec;   // [P*3] tangent render records
   float4* contrib; // [N*3] per (tile, Gaussian) reduced gradient rows
+  // The LM row map: the rows of the LM tile passes exist only for HEAD entries (list position below the
+  // largest n_contrib of their tile -- every later entry's row would be zero).  hscan[o] = number of head
+  // entries among the goff-order slots [0, o), o <= N, so Gaussian g's rows are [hscan[goff[g]],
+  // hscan[goff[g] + tiles[g]]), contiguous; each sorted head entry's row slot is hscan of its goff slot.
+  uint32_t* hscan;    // [N + 1]
+  uint32_t* scan_tmp; // block sums of the scan over N
 };
 
 size_t geom_layout(int64_t P, void* base, GeomBufs* out);
@@ -365,6 +372,8 @@ size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
 int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
 int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
+int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,
+                     int64_t N, hipStream_t s);
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s);

@@ -287,19 +287,19 @@ int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, co
                          const ScratchBufs& sb, int64_t N, const float* weight, bool mask_xyz, bool tail_clean,
                          hipStream_t s) {
   const int ntiles = v.gx * v.gy;
-  // the per-entry row slots live with the tail rows: computed by the first product on a geometry
+  // the LM row map (head entries only; ScratchBufs::hscan): computed by the first product on a geometry
   if (!tail_clean) {
-    const int st = launch_row_slots(v, gb, bb, N, s);
+    const int st = launch_lm_rowmap(v, gb, bb, ib, sb, N, s);
     if (st) return st;
   }
   if (mask_xyz)
     hipLaunchKernelGGL(k_render_matvec<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, sb.trec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib,
-                       tail_clean ? 0 : 1);
+                       0);  // no tail rows: the row map holds head entries only
   else
     hipLaunchKernelGGL(k_render_matvec<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
                        gb.rec, sb.trec, bb.slots, gb.rect, gb.goff, ib.final_T, ib.n_contrib, weight, sb.contrib,
-                       tail_clean ? 0 : 1);
+                       0);  // no tail rows: the row map holds head entries only
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -157,12 +157,13 @@ int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* g, const gslm_
 #define GSLM_STAGE_OVERWRITE 8 /* GATHER writes y instead of accumulating into it */
 #define GSLM_STAGE_SCREEN 16   /* view-sharded exchange: write this view's per-Gaussian screen-space sums to
                                   opts->screen_out (see gslm_gather_screen) instead of gathering into y */
-/* opts->flags: GSLM_MV_TAIL_CLEAN -- the caller guarantees that the scratch's gradient rows of
- * never-blended list entries (positions past every pixel's n_contrib in their tile) still hold the
- * zeros an earlier RENDER stage wrote for this same geometry / binning (no forward, backward or
- * other use of the scratch or the binning buffer since); RENDER then skips re-writing them and
- * re-deriving each sorted entry's row slot (kept in the binning buffer's free sort ping-pong half).
- * Both depend on the geometry only, so an LM step's CG loop pays for them once. */
+/* opts->flags: GSLM_MV_TAIL_CLEAN -- the caller guarantees that the LM row map an earlier RENDER stage built
+ * for this same geometry / binning is intact (no forward or drop-in backward, no other use of the scratch's map
+ * or of the binning buffer since).  The row map gives gradient rows only to HEAD list entries (positions below
+ * the largest n_contrib of their tile: every later entry's row would be zero), packed per Gaussian; it holds
+ * each sorted entry's row slot (in the binning buffer's free sort ping-pong half) and the per-Gaussian row
+ * offsets (in the scratch).  It depends on the geometry only, so an LM step's CG loop builds it once; without
+ * the flag RENDER rebuilds it. */
 #define GSLM_MV_TAIL_CLEAN 1
 /* opts->flags: GSLM_MV_SH_REST_PROJECTED -- single-view Krylov space of the SH-rest group.  With one view,
  * Gaussian i's SH-rest columns of J are B_rest(dir_i) (x) d rgb, so J^T W J + D (D a scalar on the group)
