@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
 }
 
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n,
-                                                             int shift, uint32_t* __restrict__ hist,
+                                                             int shift, uint32_t dmask, uint32_t* __restrict__ hist,
                                                              int nblocks) {
   __shared__ uint32_t cnt[RADIX];
   const int tid = threadIdx.x;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __r
 #pragma unroll 4
   for (int r = 0; r < SORT_ITEMS; ++r) {
     const int64_t i = base + r * SORT_THREADS + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (RADIX - 1)], 1u);
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
   }
   __syncthreads();
   hist[(int64_t)tid * nblocks + blockIdx.x] = cnt[tid];
@@ -97,6 +97,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
   const int nvalid = (int)min<int64_t>(SORT_TILE, n - base);
   const int wbase = w * WAVE_KEYS;
+  const uint32_t dmask = (1u << nbits) - 1u;
 
 #pragma unroll
   for (int k = 0; k < 4; ++k) s_wcnt[w][lane + 64 * k] = 0u;
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
     const bool valid = wbase + r * 64 + lane < nvalid;
-    const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+    const uint32_t d = (key[r] >> shift) & dmask;
     unsigned long long m = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
     if (wbase + r * 64 + lane < nvalid) {
-      const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+      const uint32_t d = (key[r] >> shift) & dmask;
       const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
       s_keys[lp] = key[r];
       s_vals[lp] = val[r];
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   // 3. each run to its global offset, consecutive threads on consecutive elements
   for (int e = tid; e < nvalid; e += SORT_THREADS) {
     const uint32_t k = s_keys[e];
-    const uint32_t d = (k >> shift) & (RADIX - 1);
+    const uint32_t d = (k >> shift) & dmask;
     const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_loc[d]);
     kout[pos] = k;
     vout[pos] = s_vals[e];
@@ -332,10 +333,15 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
   bool alt = false;
-  for (int shift = 0; shift < end_bit; shift += 8) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, hist, nb);
+  // ceil(end_bit / 8) passes with the bits split evenly (13-bit tile ids: 7 + 6, not 8 + 5): fewer, longer
+  // digit runs per block in the scatter (coalesced writes) for the same pass count
+  const int passes = (end_bit + 7) / 8;
+  const int per = (end_bit + passes - 1) / passes;
+  for (int shift = 0; shift < end_bit; shift += per) {
+    const int nbits = end_bit - shift < per ? end_bit - shift : per;  // digit bits of this pass
+    const uint32_t dmask = (1u << nbits) - 1u;
+    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
     hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-    const int nbits = end_bit - shift < 8 ? end_bit - shift : 8;  // digit bits of this pass (the last may be short)
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki,
                        (first && iota_values) ? (const uint32_t*)nullptr : vi, ko, vo, n, shift, nbits, hist, nb,
                        totals);
