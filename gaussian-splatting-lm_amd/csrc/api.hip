@@ -416,7 +416,7 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
     return GSLM_ERR_INVALID;
   }
   if ((stages & GSLM_STAGE_TANGENT) &&
-      (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s)))
+      (st = launch_tangent_pre(b.v, b.g, t, nullptr, b.gb, b.sb, fused_xpby ? &xp : nullptr, s, mask_xyz != 0)))
     return st;
   float* jv_out = opts ? opts->jv_out : nullptr;
   if (jv_out) {
@@ -543,7 +543,7 @@ int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussi
   const bool fused = opts && opts->xpby_s;
   if (fused && (st = build_xpby(opts, vin, R, mask_xyz != 0, &xp))) return st;
   return launch_tangent_views(vk, nviews, g, t, vflags, flags_stride, trec_out, trec_stride, fused ? &xp : nullptr,
-                              (hipStream_t)stream);
+                              (hipStream_t)stream, mask_xyz != 0);
 }
 
 int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,

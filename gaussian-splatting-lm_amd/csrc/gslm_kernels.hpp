@@ -405,8 +405,9 @@ struct XpbyK {
   const double* aden;
   int64_t xoff;
 };
+// compact: the LM rows' 8-float tangent records (store_trec, tangent.hip) instead of 12 floats
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
-                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s);
+                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s, bool compact);
 int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s);
 constexpr int MAX_SCREEN_VIEWS = 16;
 struct ViewsK {
@@ -418,7 +419,7 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
                          hipStream_t s);
 int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s);
 int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
-                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s);
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact);
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);

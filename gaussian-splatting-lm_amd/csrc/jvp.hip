@@ -53,13 +53,15 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
       s_r0[tid] = rec[3 * g + 0];
       s_r1[tid] = rec[3 * g + 1];
       const float4 r2 = rec[3 * g + 2];
-      const float4 t0 = trec[3 * g + 0], t1 = trec[3 * g + 1], t2 = trec[3 * g + 2];
       if (PACKED) {
-        // the LM product's 9 primal + 7 tangent floats as 4 float4 at one LDS stride: the hit loop reads
-        // them with one address register; the tangent conic carries its power factors (-1/2, -1, -1/2)
-        s_t0[tid] = make_float4(r2.x, -0.5f * t0.z, -t0.w, -0.5f * t1.x);  // blue, da', db', dc'
-        s_t1[tid] = make_float4(t1.y, t1.z, t1.w, t2.x);                    // dopacity, dr, dg, db
+        // the LM rows' compact tangent record (store_trec): [da db dc dop | dr dg db 0].  The product's 9 primal +
+        // 7 tangent floats as 4 float4 at one LDS stride: the hit loop reads them with one address register;
+        // the tangent conic carries its power factors (-1/2, -1, -1/2)
+        const float4 c0 = trec[2 * g + 0], c1 = trec[2 * g + 1];
+        s_t0[tid] = make_float4(r2.x, -0.5f * c0.x, -c0.y, -0.5f * c0.z);  // blue, da', db', dc'
+        s_t1[tid] = make_float4(c0.w, c1.x, c1.y, c1.z);                    // dopacity, dr, dg, db
       } else {
+        const float4 t0 = trec[3 * g + 0], t1 = trec[3 * g + 1], t2 = trec[3 * g + 2];
         s_r2[tid] = make_float2(r2.x, r2.y);
         s_t0[tid] = t0;
         s_t1[tid] = t1;
@@ -139,7 +141,8 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
   }
 }
 
-template <bool WITH_XY>
+// COMPACT: the LM rows' 8-float tangent records (xyz frozen), the colour tangent only (out_inv_t must be NULL).
+template <bool WITH_XY, bool COMPACT = false>
 __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
@@ -160,8 +163,9 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   const int64_t pid = (int64_t)py * v.W + px;
   const uint32_t last = inside ? n_contrib[pid] : 0u;
   JvpPix o;
-  jvp_tile<WITH_XY, true, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec, trec,
-                          s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
+  static_assert(!(COMPACT && WITH_XY), "compact records carry no screen-position tangent");
+  jvp_tile<WITH_XY, !COMPACT, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec,
+                                 trec, s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   if (inside) {
     const int64_t HW = (int64_t)v.H * v.W;
     out_color_t[pid] = o.dC[0] + o.dT * v.bg[0];
@@ -256,7 +260,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s) {
-  int st = launch_tangent_pre(v, g, t, m2t, gb, sb, nullptr, s);
+  int st = launch_tangent_pre(v, g, t, m2t, gb, sb, nullptr, s, false);  // the drop-in JVP: 12-float records
   if (st) return st;
   const int ntiles = v.gx * v.gy;
   const bool xy = t.means3D != nullptr || m2t != nullptr;
@@ -273,8 +277,8 @@ int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2
 int launch_render_jv(const ViewK& v, const GaussK& t, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib,
                      const ScratchBufs& sb, bool mask_xyz, float* jv_out, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
-  if (mask_xyz)
-    hipLaunchKernelGGL(k_render_jvp<false>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+  if (mask_xyz)  // the TANGENT stage of the LM rows wrote compact records
+    hipLaunchKernelGGL((k_render_jvp<false, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out, (float*)nullptr);
   else
     hipLaunchKernelGGL(k_render_jvp<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,

@@ -88,11 +88,24 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
     }
 }
 
+// Tangent render record of Gaussian i: 12 floats [dx dy da db | dc dop dr dg | db dinv 0 0] (3 float4), or for
+// the LM rows (xyz frozen, no inverse-depth term; `compact`) 8 floats [da db dc dop | dr dg db 0] (2 float4).
+__device__ __forceinline__ void store_trec(float4* __restrict__ out, int64_t i, const float T2[10], bool compact) {
+  if (compact) {
+    out[2 * i + 0] = make_float4(T2[2], T2[3], T2[4], T2[5]);
+    out[2 * i + 1] = make_float4(T2[6], T2[7], T2[8], 0.f);
+  } else {
+    out[3 * i + 0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
+    out[3 * i + 1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
+    out[3 * i + 2] = make_float4(T2[8], T2[9], 0.f, 0.f);
+  }
+}
+
 template <bool RAW, bool XPBY>
 __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
                                                          const float4* __restrict__ rec,
                                                          const uint32_t* __restrict__ tiles,
-                                                         float4* __restrict__ trec, XpbyK xp) {
+                                                         float4* __restrict__ trec, XpbyK xp, int compact) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (XPBY) {
@@ -110,14 +123,12 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
   if (tiles[i] == 0) return;  // never gathered by the render passes
   float T2[10];
   chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[3 * i + 2].z), T2);
-  trec[3 * i + 0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
-  trec[3 * i + 1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
-  trec[3 * i + 2] = make_float4(T2[8], T2[9], 0.f, 0.f);
+  store_trec(trec, i, T2, compact != 0);
 }
 
 // ------------------------------------------------------------------ launcher
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
-                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s) {
+                       const ScratchBufs& sb, const XpbyK* xp, hipStream_t s, bool compact) {
   // P = 0 with a fused direction update: one block still applies the flat tail's update (block_xpby)
   if (g.P == 0 && !(xp && xp->tail_p)) return GSLM_OK;
   const unsigned nb = (unsigned)((g.P + 255) / 256) + (g.P == 0 ? 1u : 0u);
@@ -131,17 +142,17 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
     const size_t lds = (size_t)256 * xp->w[2] * sizeof(float);
     if (g.raw)
       hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
+                         sb.trec, x, compact ? 1 : 0);
     else
       hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
+                         sb.trec, x, compact ? 1 : 0);
   } else {
     if (g.raw)
       hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
+                         sb.trec, x, compact ? 1 : 0);
     else
       hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
-                         sb.trec, x);
+                         sb.trec, x, compact ? 1 : 0);
   }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
@@ -153,7 +164,7 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
 template <bool XPBY>
 __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, GaussK t, const uint32_t* __restrict__ vflags,
                                                         int64_t fstride, float4* __restrict__ out, int64_t ostride,
-                                                        XpbyK xp) {
+                                                        XpbyK xp, int compact) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + threadIdx.x;
@@ -176,15 +187,12 @@ __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, Gaus
     if (!(f >> 31)) continue;
     float T2[10];
     chain_jvp<true>(vs.v[b], g, t, nullptr, i, f & 7u, T2);
-    float4* o = out + 3 * ((int64_t)b * ostride + i);
-    o[0] = make_float4(T2[0], T2[1], T2[2], T2[3]);
-    o[1] = make_float4(T2[4], T2[5], T2[6], T2[7]);
-    o[2] = make_float4(T2[8], T2[9], 0.f, 0.f);
+    store_trec(out, (int64_t)b * ostride + i, T2, compact != 0);
   }
 }
 
 int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
-                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s) {
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact) {
   if (nviews < 1 || nviews > MAX_SCREEN_VIEWS) {
     set_error("tangent_views: 1..16 views per call");
     return GSLM_ERR_INVALID;
@@ -202,9 +210,11 @@ int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const 
   XpbyK none{};
   float4* o = reinterpret_cast<float4*>(out);
   if (xp)
-    hipLaunchKernelGGL(k_tangent_views<true>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, *xp);
+    hipLaunchKernelGGL(k_tangent_views<true>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, *xp,
+                       compact ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_tangent_views<false>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, none);
+    hipLaunchKernelGGL(k_tangent_views<false>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, none,
+                       compact ? 1 : 0);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -174,7 +174,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 3  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 4  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):
@@ -190,7 +190,8 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
-    if lib.gslm_abi_version() != ABI_VERSION:
+    # GSLM_ABI_ANY=1: accept another ABI version whose structs are unchanged (A/B timing of an older build only)
+    if lib.gslm_abi_version() != ABI_VERSION and os.environ.get("GSLM_ABI_ANY") != "1":
         raise ImportError(f"{LIB_PATH} has C ABI version {lib.gslm_abi_version()}, these bindings need "
                           f"{ABI_VERSION}: rebuild it")
     return lib

@@ -193,13 +193,13 @@ class GaussianShardedOperator:
     every CG vector (x, s, p, q and J^T b are shard-sized, `layout`) and the per-Gaussian work on them.
     Per product (matvec_dot), with b = (k, t) running over every view (k-th view of rank t):
       1. gslm_tangent_views: this shard's tangent render records for every view (the fused direction
-         update p = s + beta p [, x += alpha p] on the shard first) -> trec[k][t][S][12];
+         update p = s + beta p [, x += alpha p] on the shard first) -> trec[k][t][S][8];
       2. all_to_all per k: rank t receives every shard's records of its k-th view = a [P][12] table;
       3. RENDER | SCREEN with opts.trec_in: the view's fused JVP -> VJP tile pass and row sums -> [P][8];
       4. all_to_all per k: rank r receives the [S][8] slices of its shard from every view;
       5. gslm_gather_screen over the shard, every view's chain, + D v, <v, y> partial.
     The CG scalars are sums over shards: one small all-reduce each (DEL, GAMN [, monitor dots]) via
-    `allreduce_scalars`, which gslm.lm.cgls_fused calls.  A rank receives (48 + 32) (n - 1) / n bytes per
+    `allreduce_scalars`, which gslm.lm.cgls_fused calls.  A rank receives (32 + 32) (n - 1) / n bytes per
     Gaussian per view instead of the screen all-gather's 32 (n - 1), and runs 1/n of the chains, gathers
     and vector algebra.  J^T b and the loss are all-reduced once per LM step (full layout), then sliced.
 
@@ -381,8 +381,9 @@ class GaussianShardedOperator:
             self._bufs = dict(
                 flags_local=torch.zeros(per, n * S, dtype=torch.int32, device=dev),
                 flags=torch.zeros(per, n * S, dtype=torch.int32, device=dev),
-                trec_send=torch.zeros(per, n * S, 12, dtype=torch.float32, device=dev),
-                trec_recv=torch.zeros(per, n * S, 12, dtype=torch.float32, device=dev),
+                # the LM rows' compact tangent records: 8 floats per Gaussian (gslm_tangent_views with mask_xyz)
+                trec_send=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev),
+                trec_recv=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev),
                 screen_send=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev),
                 screen_recv=torch.zeros(per, n * S, 8, dtype=torch.float32, device=dev))
         return self._bufs
@@ -443,7 +444,7 @@ class GaussianShardedOperator:
             vptr = ctypes.cast(ctypes.byref(self.views_kt, c0 * vsz), ctypes.POINTER(_lib.GslmView))
             check(lib.gslm_tangent_views(vptr, c1 - c0, ctypes.byref(gs), ctypes.byref(vs), int(self.mask_xyz),
                                          b["flags"].data_ptr() + 4 * c0 * S, S,
-                                         b["trec_send"].data_ptr() + 48 * c0 * S, S,
+                                         b["trec_send"].data_ptr() + 32 * c0 * S, S,
                                          None if opts is None else ctypes.byref(opts), loc.stream),
                   "gslm_tangent_views")
         # 2. every shard's records of my k-th view

@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 3
+#define GSLM_ABI_VERSION 4
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -210,8 +210,8 @@ typedef struct gslm_matvec_opts {
   const double* alpha_den;
   int64_t xpby_x_offset;
   /* Gaussian-sharded exchange (gslm_tangent_views below): when set, RENDER reads this view's tangent render
-   * records ([>= P][12] floats, gslm_tangent_views' output once exchanged) instead of the TANGENT stage's
-   * (TANGENT must be off). */
+   * records (gslm_tangent_views' output once exchanged: [>= P][8] floats with mask_xyz, [>= P][12] without)
+   * instead of the TANGENT stage's (TANGENT must be off). */
   const float* trec_in;
   /* gslm_gather_screen only: Gaussians between consecutive views' blocks of screen (0 means P). */
   int64_t screen_stride;
@@ -255,8 +255,10 @@ int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussi
  * gslm_view_flags: out[i] = 0 if Gaussian i touches no tile of the preprocessed view, else
  * 0x80000000 | its 3 SH-clamp bits (the flags word of the SCREEN rows); exchanged once per geometry. */
 int gslm_view_flags(const void* geom, int64_t P, uint32_t* out, void* stream);
-/* trec_out[(b trec_stride + i) * 12 ..] = tangent render record of shard Gaussian i in view b where
- * vflags[b flags_stride + i] is visible (other records untouched), b < nviews (<= 16).  g / v: the shard's
+/* trec_out[(b trec_stride + i) * R ..] = tangent render record of shard Gaussian i in view b where
+ * vflags[b flags_stride + i] is visible (other records untouched), R = 8 floats with mask_xyz (the LM rows:
+ * [da db dc dop | dr dg db 0], the conic / opacity / colour tangents) or 12 without
+ * ([dx dy da db | dc dop dr dg | db dinv 0 0]), b < nviews (<= 16).  g / v: the shard's
  * leaves and direction (P = shard size, SH-rest stride 3(M-1)); opts (or NULL): only the fused direction
  * update (xpby_s, beta_*, alpha_*, xpby_x_offset, xpby_tail_*) of gslm_matvec_view_ex, applied once before
  * the views' tangents.  The flat tail (xpby_tail_*) is updated once per call, so it must be this rank's

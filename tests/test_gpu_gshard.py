@@ -60,14 +60,14 @@ def test_gaussian_sharded_product_matches_unsharded():
     views = prob.views_for(cams)
     g = raw_gaussians(m)
     vs = prob.layout.grads_struct(v)
-    trec = torch.zeros(n, P, 12, device="cuda")
+    trec = torch.zeros(n, P, 8, device="cuda")  # the LM rows' compact records (mask_xyz)
     cut = (P * 3) // 7  # not a multiple of the 256-Gaussian block
     shards = [(0, cut), (cut, P)]
     for s0, s1 in shards:
         gs = _slice(g, _lib.GslmGaussians, s0, s1, R, True)
         vss = _slice(vs, _lib.GslmGrads, s0, s1, R, False)
         check(lib.gslm_tangent_views(views, n, ctypes.byref(gs), ctypes.byref(vss), 1,
-                                     flags.data_ptr() + 4 * s0, P, trec.data_ptr() + 48 * s0, P, None,
+                                     flags.data_ptr() + 4 * s0, P, trec.data_ptr() + 32 * s0, P, None,
                                      prob.stream), "gslm_tangent_views")
     got = torch.zeros(n, P, 8, device="cuda")
     for b, vr in enumerate(prob.views):
@@ -174,7 +174,7 @@ def test_tangent_views_fused_direction_update_matches_tangent_stage():
     flags = torch.zeros(n, P, dtype=torch.int32, device="cuda")
     for b, vr in enumerate(prob.views):
         check(lib.gslm_view_flags(vr.geom.data_ptr(), P, flags[b].data_ptr(), prob.stream), "gslm_view_flags")
-    trec = torch.zeros(n, P, 12, device="cuda")
+    trec = torch.zeros(n, P, 8, device="cuda")
     cut = (P * 3) // 7
     shards = [(0, cut), (cut, P)]
     p_out, x_out = p0.clone(), xv0.clone()
@@ -187,7 +187,7 @@ def test_tangent_views_fused_direction_update_matches_tangent_stage():
         gs = _slice(g, _lib.GslmGaussians, s0, s1, R, True)
         vss = _slice(lay.grads_struct(p_sh), _lib.GslmGrads, s0, s1, R, False)
         check(lib.gslm_tangent_views(views, n, ctypes.byref(gs), ctypes.byref(vss), 1,
-                                     flags.data_ptr() + 4 * s0, P, trec.data_ptr() + 48 * s0, P, ctypes.byref(opts),
+                                     flags.data_ptr() + 4 * s0, P, trec.data_ptr() + 32 * s0, P, ctypes.byref(opts),
                                      prob.stream), "gslm_tangent_views")
         torch.cuda.synchronize()
         pv, xv, po, xo = lay.views(p_sh), lay.views(x_sh), lay.views(p_out), lay.views(x_out)
@@ -255,7 +255,7 @@ def test_render_gather_from_trec_in_matches_full_product(mask_xyz):
     ref = product(7)
     flags = torch.zeros(P, dtype=torch.int32, device="cuda")
     check(lib.gslm_view_flags(vr.geom.data_ptr(), P, flags.data_ptr(), prob.stream), "gslm_view_flags")
-    trec = torch.zeros(P, 12, device="cuda")
+    trec = torch.zeros(P, 8 if mask_xyz else 12, device="cuda")
     views = prob.views_for(cams[:1])
     check(lib.gslm_tangent_views(views, 1, ctypes.byref(g), ctypes.byref(vs), mask_xyz, flags.data_ptr(), P,
                                  trec.data_ptr(), P, None, prob.stream), "gslm_tangent_views")

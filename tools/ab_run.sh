@@ -6,7 +6,7 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for L in "$@"; do
-  GSLM_LIB=$PWD/gaussian-splatting-lm_amd/$L/libgslm.so timeout -k 10 240 python tools/mv_ab.py $L --out /tmp/gslm_ab \
+  GSLM_ABI_ANY=1 GSLM_LIB=$PWD/gaussian-splatting-lm_amd/$L/libgslm.so timeout -k 10 240 python tools/mv_ab.py $L --out /tmp/gslm_ab \
     > $OUT/$L.json 2> $OUT/$L.err || { tail -5 $OUT/$L.err; exit 1; }
   cat $OUT/$L.json
 done
