@@ -65,6 +65,14 @@ __device__ __forceinline__ float wave_reduce8_t(const float v[8], int lane) {
   return x;                 // value index of this lane: (lane >> 3) & 7
 }
 
+// Orders a wave's LDS stores before its later loads of other lanes' slots (a wave's LDS operations complete in
+// order; this only stops the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Block-wide count of `pred` over 256 threads (4 waves) with one barrier; s_cnt = 4 ints of LDS the
 // caller owns.  Replaces __syncthreads_count, whose lowering reserves 256 B of LDS per block -- the
 // difference between 3 and 4 resident blocks per CU for k_render_matvec.  Safe to call once per

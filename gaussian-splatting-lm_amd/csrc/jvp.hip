@@ -6,6 +6,8 @@
 //                        dC += drgb a T + rgb (da T + a dT),  dT <- dT (1 - a) - T da.
 //   k_render_matvec    the fused pair: JVP pass -> u = 2 w (.) J v in registers -> VJP pass ->
 //                      one reduced row per (tile, Gaussian); the per-pixel J v never touches HBM.
+//                      With the compact LM records the JVP pass runs one independent wave per quadrant
+//                      (jvp_wave_packed, no block barrier; k_render_jv_wave is the J v-only form).
 #include "gslm_tile.hpp"
 #include "gslm_chain.hpp"
 
@@ -141,6 +143,92 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
   }
 }
 
+// Front-to-back tangent pass of ONE wave over its 8x8 quadrant q, independent of the tile's other waves (no
+// block barrier): 64 list positions per round, each lane fetches one; the entries whose quadrant mask holds q
+// stage the compact LM record in the wave's own LDS slots (lane-indexed), and the wave walks the round's hit
+// bits in list order.  Same per-lane arithmetic and decisions as jvp_tile's PACKED branch.
+__device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf, uint32_t my_last, int wm, int q,
+                                                const uint32_t* __restrict__ pl, const float4* __restrict__ rec,
+                                                const float4* __restrict__ trec, float4* s) {
+  const int lane = threadIdx.x & 63;
+  o.T = 1.f;
+  o.dT = 0.f;
+  o.dC[0] = o.dC[1] = o.dC[2] = 0.f;
+  o.dD = 0.f;
+  for (int base = 0; base < wm; base += 64) {
+    const int k = base + lane;
+    bool hit = false;
+    if (k < wm) {
+      const uint32_t e = pl[k];
+      if ((pl_mask(e) >> q) & 1u) {
+        hit = true;
+        const uint32_t g = pl_id(e);
+        const float4 r0 = rec[3 * (size_t)g + 0], r1 = rec[3 * (size_t)g + 1], r2 = rec[3 * (size_t)g + 2];
+        const float4 c0 = trec[2 * (size_t)g + 0], c1 = trec[2 * (size_t)g + 1];
+        s[lane] = r0;
+        s[64 + lane] = r1;
+        s[128 + lane] = make_float4(r2.x, -0.5f * c0.x, -c0.y, -0.5f * c0.z);  // blue, da', db', dc'
+        s[192 + lane] = make_float4(c0.w, c1.x, c1.y, c1.z);                    // dopacity, dr, dg, db
+      }
+    }
+    uint64_t hb = __ballot(hit);
+    wave_lds_sync();
+    while (hb) {
+      const int j = (int)__builtin_ctzll(hb);
+      hb &= hb - 1ull;
+      const float4 a = s[j], b = s[64 + j], C = s[128 + j], D = s[192 + j];
+      asm volatile("" : : "v"(b.z), "v"(b.w), "v"(C.x), "v"(C.y), "v"(C.z), "v"(C.w), "v"(D.x), "v"(D.y), "v"(D.z),
+                   "v"(D.w));
+      const uint32_t pos = (uint32_t)(base + j);
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float G = gexp(power);
+      const float alpha = fminf(0.99f, b.y * G);
+      if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+#pragma clang fp contract(fast)
+        const float dpower = (C.y * dx * dx + C.w * dy * dy) + C.z * dx * dy;
+        const float dalpha = G * (D.x + b.y * dpower);
+        const float wt = alpha * o.T;
+        const float dw = dalpha * o.T + alpha * o.dT;
+        o.dC[0] += D.y * wt + b.z * dw;
+        o.dC[1] += D.z * wt + b.w * dw;
+        o.dC[2] += D.w * wt + C.x * dw;
+        o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
+        o.T = o.T * (1.f - alpha);
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+// J v only, compact LM records, one independent wave per quadrant (jvp_wave_packed).
+__global__ __launch_bounds__(256) void k_render_jv_wave(ViewK v, const uint2* __restrict__ ranges,
+                                                         const uint32_t* __restrict__ tile_order,
+                                                         const uint32_t* __restrict__ point_list,
+                                                         const float4* __restrict__ rec, const float4* __restrict__ trec,
+                                                         const uint32_t* __restrict__ n_contrib,
+                                                         float* __restrict__ out_color_t) {
+  __shared__ float4 s_rec[4][4 * 64];
+  const int tile = (int)tile_order[blockIdx.x];
+  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
+  const int tid = threadIdx.x, q = tid >> 6;
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
+  const bool inside = px < v.W && py < v.H;
+  const int64_t pid = (int64_t)py * v.W + px;
+  const uint32_t last = inside ? n_contrib[pid] : 0u;
+  const uint2 range = ranges[tile];
+  const int wm = __builtin_amdgcn_readfirstlane(min(wave_max_u((int)last), (int)(range.y - range.x)));
+  JvpPix o;
+  jvp_wave_packed(o, (float)px, (float)py, last, wm, q, point_list + range.x, rec, trec, s_rec[q]);
+  if (inside) {
+    const int64_t HW = (int64_t)v.H * v.W;
+    out_color_t[pid] = o.dC[0] + o.dT * v.bg[0];
+    out_color_t[HW + pid] = o.dC[1] + o.dT * v.bg[1];
+    out_color_t[2 * HW + pid] = o.dC[2] + o.dT * v.bg[2];
+  }
+}
+
 // COMPACT: the LM rows' 8-float tangent records (xyz frozen), the colour tangent only (out_inv_t must be NULL).
 template <bool WITH_XY, bool COMPACT = false>
 __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __restrict__ ranges,
@@ -191,21 +279,25 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   // 128-entry batches: 19.7 KB of LDS per block -> 8 blocks (VGPR-limited to 6 waves per SIMD) per CU,
   // the occupancy this latency-bound pass needs
   constexpr int B = MATVEC_BATCH;
-  __shared__ float4 s_r0[B], s_r1[B];
-  __shared__ float2 s_r2[B];
   __shared__ uint64_t s_bits[16];
   __shared__ int s_cnt[4];
-  // The JVP pass's tangent records and the VJP pass's per-wave partials (+ its n_eff scratch) are
-  // never live together (vjp_tile starts with a block barrier): one LDS region.
-  constexpr int kAcc = vjp_acc_floats<WITH_XY, false, B>();
-  constexpr int kTan = (4 + 4 + 2) * B;
-  constexpr int kU = ((kAcc > kTan ? kAcc : kTan) + 3) / 4;
-  __shared__ float4 s_union[kU];
-  float4* s_t0 = s_union;
-  float4* s_t1 = s_union + B;
-  float2* s_t2 = reinterpret_cast<float2*>(s_union + 2 * B);
-  float* s_acc = reinterpret_cast<float*>(s_union);
-  int* s_misc = reinterpret_cast<int*>(s_union);
+  // The JVP pass's records and the VJP pass's staged records, per-wave partials (+ its n_eff scratch) are never
+  // live together (vjp_tile starts with a block barrier): one LDS region.  Without screen-position tangents
+  // the JVP pass runs one independent wave per quadrant (jvp_wave_packed: 4 x 256 float4 of wave-private
+  // records); with them the block-cooperative jvp_tile.
+  constexpr int kAcc = (vjp_acc_floats<WITH_XY, false, B>() + 3) / 4;  // float4
+  constexpr int kVjp = kAcc + B + B + B / 2;                             // + s_r0, s_r1, s_r2
+  constexpr int kJvp = WITH_XY ? 0 : 4 * 256;
+  static_assert(!WITH_XY || kAcc >= 2 * B + B / 2, "jvp_tile's tangent records must fit below s_r0");
+  __shared__ float4 s_lds[kVjp > kJvp ? kVjp : kJvp];
+  float* s_acc = reinterpret_cast<float*>(s_lds);
+  int* s_misc = reinterpret_cast<int*>(s_lds);
+  float4* s_r0 = s_lds + kAcc;
+  float4* s_r1 = s_r0 + B;
+  float2* s_r2 = reinterpret_cast<float2*>(s_r1 + B);
+  float4* s_t0 = s_lds;  // jvp_tile's tangent records (WITH_XY), below s_r0
+  float4* s_t1 = s_t0 + B;
+  float2* s_t2 = reinterpret_cast<float2*>(s_t1 + B);
   const int tile = (int)tile_order[blockIdx.x];
 #ifdef GSLM_EXPERIMENT_TIMELINE
   if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile] = wall_clock64();
@@ -231,8 +323,15 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
 #ifdef GSLM_EXPERIMENT_SKIP_JVP
   o.dC[0] = o.dC[1] = o.dC[2] = o.dT = 1e-3f;
 #else
-  jvp_tile<WITH_XY, false, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
-                           s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
+  if constexpr (WITH_XY) {
+    jvp_tile<WITH_XY, false, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
+                                s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
+  } else {
+    const int q = tid >> 6;
+    const int wm = __builtin_amdgcn_readfirstlane(min(wave_max_u(inside ? (int)last : 0), (int)(range.y - range.x)));
+    jvp_wave_packed(o, (float)px, (float)py, inside ? last : 0u, wm, q, point_list + range.x, rec, trec,
+                    s_lds + 256 * q);
+  }
 #endif
   // u = 2 * w (.) (J v)   -- factor 2: the [r; r] residual aliasing of batch_training_loss.py:17
   const float u0 = 2.f * w0 * (o.dC[0] + o.dT * v.bg[0]);
@@ -278,8 +377,8 @@ int launch_render_jv(const ViewK& v, const GaussK& t, const GeomBufs& gb, const 
                      const ScratchBufs& sb, bool mask_xyz, float* jv_out, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (mask_xyz)  // the TANGENT stage of the LM rows wrote compact records
-    hipLaunchKernelGGL((k_render_jvp<false, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
-                       bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out, (float*)nullptr);
+    hipLaunchKernelGGL(k_render_jv_wave, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out);
   else
     hipLaunchKernelGGL(k_render_jvp<true>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, sb.trec, ib.n_contrib, jv_out, (float*)nullptr);

@@ -73,9 +73,13 @@ def main():
     vs = prob.layout.grads_struct(g)
     ys = prob.layout.grads_struct(prob.zeros(), accumulate=True)
 
-    def stage(mask):
+    jv = torch.zeros(3, H, W, device=dev)
+
+    def stage(mask, jv_out=False):
         opts = _lib.GslmMatvecOpts()
         opts.stages = mask | (8 if mask == 4 else 0)
+        if jv_out:
+            opts.jv_out = jv.data_ptr()
         opts.flags = 1 | prob.mv_flags
         opts.damp7 = prob._damps if mask == 4 else None
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
@@ -97,6 +101,7 @@ def main():
     res["tangent_ms"] = ev(lambda: stage(1), a.reps)
     res["render_matvec_ms"] = ev(lambda: stage(2), a.reps)
     res["gather_ms"] = ev(lambda: stage(4), a.reps)
+    res["jv_ms"] = ev(lambda: stage(2, jv_out=True), a.reps)
     cgls_fused(prob, g, max_iter=2, restart_iter=2, check_every=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -111,7 +116,7 @@ def main():
     torch.cuda.synchronize()
     res["forward_ms"] = 1e3 * (time.perf_counter() - t0) / a.reps
     os.makedirs(a.out, exist_ok=True)
-    torch.save({"y": y.cpu(), "color": vr.color.cpu()}, os.path.join(a.out, a.tag + ".pt"))
+    torch.save({"y": y.cpu(), "color": vr.color.cpu(), "jv": jv.cpu()}, os.path.join(a.out, a.tag + ".pt"))
     print(json.dumps(res), flush=True)
 
 
