@@ -257,16 +257,23 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           cd = (b.z * st.dpix[0] + b.w * st.dpix[1]) + c.x * st.dpix[2];
           if (WITH_INV) cd += c.y * st.dinv;
         }
+        // A visit some lane blends runs the body in every lane, an invalid lane with alpha = G = 0: its row
+        // values are 0, T is unchanged (rcp(1) = 1), and the pending <acc, u> update it applies early is the
+        // one the next blended entry would apply with the same operands (it then adds 0 * (...)).  No
+        // per-lane branch and no zeroing of the row values per visit.
+        const bool any = __ballot(valid) != 0ull;
         float gv[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) gv[q] = 0.f;
-        if (valid) {
+        const float a_e = valid ? alpha : 0.f;
+        const float G_e = valid ? G : 0.f;
+        if (any) {
           // Only the primal tests above (power, alpha) must round exactly as the forward's; the
           // derivative arithmetic below decides nothing and is contracted to FMAs.
 #pragma clang fp contract(fast)
-          const float inv1ma = rcp_f(1.f - alpha);
+          const float inv1ma = rcp_f(1.f - a_e);
           st.T = st.T * inv1ma;
-          const float dchannel = alpha * st.T;
+          const float dchannel = a_e * st.T;
           st.accd = st.accd + st.last_alpha * (st.last_cd - st.accd);
           st.last_cd = cd;
 #pragma unroll
@@ -274,8 +281,8 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           if (WITH_INV) gv[9] = dchannel * st.dinv;
           // dL/dalpha = (<c, u> - acc) T - T_final / (1 - alpha) <bg, u>   (tb = -T_final <bg, u>)
           const float dL_dalpha = (cd - st.accd) * st.T + st.tb * inv1ma;
-          st.last_alpha = alpha;
-          gv[5] = G * dL_dalpha;
+          st.last_alpha = a_e;
+          gv[5] = G_e * dL_dalpha;
           // h = G dL/dG with G = exp(power): dL/dpower = h; the conic rows carry h dx^2, h dx dy, h dy^2
           // and their constant factors (-1/2, -1, -1/2) are applied once per row at the combine
           const float h = b.y * gv[5];
@@ -288,7 +295,6 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           gv[3] = hdx * dy;
           gv[4] = hdy * dy;
         }
-        const bool any = __ballot(valid) != 0ull;
 #ifdef GSLM_EXPERIMENT_COUNT
         {
           const uint64_t vb = __ballot(valid);
