@@ -90,12 +90,94 @@ __global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __rest
   }
 }
 
+// The same blend with one independent wave per 8x8 quadrant: 64 list positions per round, each lane fetches
+// one, the entries whose mask holds the quadrant stage their record in the wave's own LDS slots (lane-indexed),
+// and the wave walks the round's hit bits in list order.  No block barrier: a wave leaves as soon as all of
+// its pixels have stopped, however far the tile's other quadrants still go.  Per-lane arithmetic and
+// decisions as k_render_fwd.
+__global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ tile_order,
+                                                          const uint32_t* __restrict__ point_list,
+                                                          const float4* __restrict__ rec, float* __restrict__ out_color,
+                                                          float* __restrict__ out_invdepth, float* __restrict__ final_T,
+                                                          uint32_t* __restrict__ n_contrib) {
+  __shared__ float4 s_rec[4][3 * 64];
+  const int tile = (int)tile_order[blockIdx.x];
+  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
+  const int tid = threadIdx.x, q = tid >> 6, lane = tid & 63;
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
+  const bool inside = px < v.W && py < v.H;
+  const float pxf = (float)px, pyf = (float)py;
+  bool done = !inside;
+  const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
+  const uint32_t* pl = point_list + range.x;
+  float4* s = s_rec[q];
+
+  float T = 1.0f;
+  uint32_t last = 0;
+  float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+  for (int base = 0; base < n; base += 64) {
+    if (__ballot(!done) == 0ull) break;  // every pixel of this quadrant has stopped
+    const int k = base + lane;
+    bool hit = false;
+    if (k < n) {
+      const uint32_t e = pl[k];
+      if ((pl_mask(e) >> q) & 1u) {
+        hit = true;
+        const uint32_t g = pl_id(e);
+        s[lane] = rec[3 * (size_t)g + 0];
+        s[64 + lane] = rec[3 * (size_t)g + 1];
+        s[128 + lane] = rec[3 * (size_t)g + 2];
+      }
+    }
+    uint64_t hb = __ballot(hit);
+    wave_lds_sync();
+    while (hb) {
+      const int j = (int)__builtin_ctzll(hb);
+      hb &= hb - 1ull;
+      const float4 a = s[j], b = s[64 + j], cc = s[128 + j];
+      asm volatile("" : : "v"(b.z), "v"(b.w), "v"(cc.x), "v"(cc.y));
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float alpha = fminf(0.99f, b.y * gexp(power));
+      const float test_T = T * (1.0f - alpha);
+      if (!done && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+        if (test_T < 0.0001f) {
+          done = true;
+        } else {
+          const float wt = alpha * T;
+          C0 += b.z * wt;
+          C1 += b.w * wt;
+          C2 += cc.x * wt;
+          Dp += cc.y * wt;
+          T = test_T;
+          last = (uint32_t)(base + j + 1);  // 1-based list position
+        }
+      }
+      if (__ballot(!done) == 0ull) break;
+    }
+    wave_lds_sync();
+  }
+  if (inside) {
+    const int64_t pid = (int64_t)py * v.W + px;
+    const int64_t HW = (int64_t)v.H * v.W;
+    final_T[pid] = T;
+    n_contrib[pid] = last;
+    out_color[pid] = C0 + T * v.bg[0];
+    out_color[HW + pid] = C1 + T * v.bg[1];
+    out_color[2 * HW + pid] = C2 + T * v.bg[2];
+    if (out_invdepth) out_invdepth[pid] = Dp;
+  }
+}
+
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_render_fwd, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list, gb.rec,
-                     out_color, out_invdepth, ib.final_T, ib.n_contrib);
+  hipLaunchKernelGGL(k_render_fwd_wave, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
+                     gb.rec, out_color, out_invdepth, ib.final_T, ib.n_contrib);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
