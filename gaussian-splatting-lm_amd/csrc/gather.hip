@@ -81,8 +81,10 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
   }
 }
 
+// 5 waves per SIMD (96 VGPRs, a few chain temporaries spilled) over the 4 the unconstrained 117 VGPRs allow:
+// the kernel is latency-bound (row sums, then the parameters, then the vector groups): 76 -> 71 us at 1M
 template <bool WANT_MEANS, int ROWF4>
-__global__ __launch_bounds__(256) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
+__global__ __launch_bounds__(256, 5) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
                                                     const uint32_t* __restrict__ hscan,
