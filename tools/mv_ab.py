@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--out", default="/tmp/gslm_ab")
     ap.add_argument("--compare", nargs="+")
     ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--ramp", type=int, default=0, help="also time N single CG iterations back to back (clock ramp)")
     a = ap.parse_args()
     if a.compare:
         compare(a.compare[0], a.compare[1:])
@@ -102,12 +103,36 @@ def main():
     res["render_matvec_ms"] = ev(lambda: stage(2), a.reps)
     res["gather_ms"] = ev(lambda: stage(4), a.reps)
     res["jv_ms"] = ev(lambda: stage(2, jv_out=True), a.reps)
+    # k_render_matvec as the CG loop runs it: between the tangent and gather passes, which stream the vectors
+    # through the caches (the back-to-back timing above replays it with its inputs cache-warm)
+    evs = []
+    for _ in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        stage(1)
+        e0.record()
+        stage(2)
+        e1.record()
+        stage(4)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    res["render_matvec_loop_ms"] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.reps
     cgls_fused(prob, g, max_iter=2, restart_iter=2, check_every=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     cgls_fused(prob, g, max_iter=a.reps, restart_iter=a.reps, check_every=False)
     torch.cuda.synchronize()
     res["cg_iter_ms"] = 1e3 * (time.perf_counter() - t0) / a.reps
+    if a.ramp:
+        # per-iteration device time of N consecutive CG iterations, launched without host syncs
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.ramp)]
+        for e0, e1 in evs:
+            e0.record()
+            cgls_fused(prob, g, max_iter=1, restart_iter=1, check_every=False)
+            e1.record()
+        torch.cuda.synchronize()
+        ts = [e0.elapsed_time(e1) for e0, e1 in evs]
+        res["ramp_ms"] = [round(t, 4) for t in ts[:5]] + [round(sum(ts[i:i + 25]) / len(ts[i:i + 25]), 4)
+                                                          for i in range(5, len(ts), 25)]
     vr.forward(graw, prob.stream)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
