@@ -81,14 +81,18 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
   }
 }
 
-// 5 waves per SIMD (96 VGPRs, a few chain temporaries spilled) over the 4 the unconstrained 117 VGPRs allow:
-// the kernel is latency-bound (row sums, then the parameters, then the vector groups): 76 -> 71 us at 1M
-template <bool WANT_MEANS, int ROWF4>
-__global__ __launch_bounds__(256, 5) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
+// PROJ: the projected SH-rest layout (FlatK::rest_proj) as a compile-time fact, which drops the full layout's
+// SH-rest epilogue from the code: at 5 waves per SIMD (96 VGPRs) over the 4 the unconstrained register count
+// allows it runs 76 -> 71 us at 1M (the kernel is latency-bound: row sums, then the parameters, then the
+// vector groups).  The full-layout variant keeps the compiler's register count: forced to 96 VGPRs its SH-rest
+// epilogue spills and takes 0.18 -> 0.31 ms.
+template <bool WANT_MEANS, int ROWF4, bool PROJ>
+__global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
                                                     const uint32_t* __restrict__ hscan,
                                                     const float4* __restrict__ rows, FlatK o) {
+  o.rest_proj = PROJ ? 1 : 0;  // the launcher picked the variant from it
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // row chunks, then the factored SH stage
   __shared__ double s_dot[4];
   const int tid = threadIdx.x;
@@ -203,11 +207,17 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
   const size_t rest_lds = sh_stage_floats<true>(g.M) * sizeof(float);
   const size_t chunk_lds = (size_t)GATHER_CHUNK * (mask_xyz ? 2 : 3) * sizeof(float4);
   const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
-  if (mask_xyz)
-    hipLaunchKernelGGL((k_gather_lm<false, 2>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+  if (mask_xyz && o.rest_proj)
+    hipLaunchKernelGGL((k_gather_lm<false, 2, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.hscan, sb.contrib, o);
+  else if (mask_xyz)
+    hipLaunchKernelGGL((k_gather_lm<false, 2, false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+                       sb.hscan, sb.contrib, o);
+  else if (o.rest_proj)
+    hipLaunchKernelGGL((k_gather_lm<true, 3, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   else
-    hipLaunchKernelGGL((k_gather_lm<true, 3>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL((k_gather_lm<true, 3, false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

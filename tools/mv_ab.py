@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--out", default="/tmp/gslm_ab")
     ap.add_argument("--compare", nargs="+")
     ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--full", action="store_true", help="the reference's full SH-rest layout (no projection)")
+    ap.add_argument("--stagger", type=int, nargs="*", default=[],
+                    help="also time the gather with its output vector offset by K floats (HBM channel alignment)")
     ap.add_argument("--ramp", type=int, default=0, help="also time N single CG iterations back to back (clock ramp)")
     a = ap.parse_args()
     if a.compare:
@@ -62,7 +65,7 @@ def main():
     cams[0].original_image = gp.views[0].color.clamp(0, 1).clone()
     del gp, pert
     model = synthetic_gaussians(a.P, 3, seed=0, s0=0.005, device="cpu", n_cams=1).to(dev)
-    prob = LMProblem(model, cams, torch.zeros(3), device=dev, sh_projection="auto")
+    prob = LMProblem(model, cams, torch.zeros(3), device=dev, sh_projection=False if a.full else "auto")
     prob.evaluate()
     g = prob.rhs(prob.zeros())
     y = prob.zeros()
@@ -102,6 +105,17 @@ def main():
     res["tangent_ms"] = ev(lambda: stage(1), a.reps)
     res["render_matvec_ms"] = ev(lambda: stage(2), a.reps)
     res["gather_ms"] = ev(lambda: stage(4), a.reps)
+    for k in a.stagger:
+        ybuf = torch.zeros(prob.layout.numel + k, dtype=torch.float32, device=dev)
+        vbuf = torch.zeros(prob.layout.numel + 2 * k, dtype=torch.float32, device=dev)
+        vbuf[2 * k:].copy_(g)
+        ys_save, vs_save = ys, vs
+        ys = prob.layout.grads_struct(ybuf[k:], accumulate=True)
+        res[f"gather_ms_ystagger{k}"] = ev(lambda: stage(4), a.reps)
+        vs = prob.layout.grads_struct(vbuf[2 * k:])
+        res[f"gather_ms_yvstagger{k}"] = ev(lambda: stage(4), a.reps)
+        ys, vs = ys_save, vs_save
+        del ybuf, vbuf
     res["jv_ms"] = ev(lambda: stage(2, jv_out=True), a.reps)
     # k_render_matvec as the CG loop runs it: between the tangent and gather passes, which stream the vectors
     # through the caches (the back-to-back timing above replays it with its inputs cache-warm)
@@ -141,7 +155,7 @@ def main():
     torch.cuda.synchronize()
     res["forward_ms"] = 1e3 * (time.perf_counter() - t0) / a.reps
     os.makedirs(a.out, exist_ok=True)
-    torch.save({"y": y.cpu(), "color": vr.color.cpu(), "jv": jv.cpu()}, os.path.join(a.out, a.tag + ".pt"))
+    torch.save({"y": y.cpu(), "color": vr.color.cpu(), "jv": jv.cpu(), "image": vr.image.cpu()}, os.path.join(a.out, a.tag + ".pt"))
     print(json.dumps(res), flush=True)
 
 
