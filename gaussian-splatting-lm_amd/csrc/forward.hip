@@ -158,17 +158,6 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
 // of gathering goff / rect per entry.  The goff / rect gathers here are random over 12 B/Gaussian
 // (~90 us at 1M Gaussians / 4.9M entries), so the fused LM product computes the slots once per
 // geometry (GSLM_MV_TAIL_CLEAN protocol) and the forward does not.
-__global__ __launch_bounds__(256) void k_row_slots(int64_t N, int gx, const uint32_t* __restrict__ keys,
-                                                    const uint32_t* __restrict__ point_list,
-                                                    const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
-                                                    uint32_t* __restrict__ slots) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= N) return;
-  const uint32_t t = keys[k];
-  const uint32_t g = pl_id(point_list[k]);
-  slots[k] = row_slot(goff[g], rect[g], (int)(t % (uint32_t)gx), (int)(t / (uint32_t)gx));
-}
-
 // ---- the LM row map (ScratchBufs::hscan), once per geometry ----
 // largest n_contrib over each tile's pixels: list positions at or past it are blended by no pixel of the tile
 __global__ __launch_bounds__(256) void k_tile_neff(ViewK v, const uint32_t* __restrict__ n_contrib,
@@ -222,14 +211,6 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
   const int st = exclusive_scan_u32(sb.hscan, nullptr, sb.hscan, N, sb.scan_tmp, sb.hscan + N, s);
   if (st) return st;
   hipLaunchKernelGGL(k_row_final, dim3(nb), dim3(256), 0, s, N, sb.hscan, bb.slots);
-  GSLM_LAUNCH_CHECK();
-  return GSLM_OK;
-}
-
-int launch_row_slots(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s) {
-  if (N <= 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_row_slots, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, v.gx, bb.keys_sorted,
-                     bb.point_list, gb.goff, gb.rect, bb.slots);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -229,8 +229,7 @@ __global__ __launch_bounds__(256) void k_render_jv_wave(ViewK v, const uint2* __
   }
 }
 
-// COMPACT: the LM rows' 8-float tangent records (xyz frozen), the colour tangent only (out_inv_t must be NULL).
-template <bool WITH_XY, bool COMPACT = false>
+template <bool WITH_XY>
 __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
@@ -251,8 +250,7 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
   const int64_t pid = (int64_t)py * v.W + px;
   const uint32_t last = inside ? n_contrib[pid] : 0u;
   JvpPix o;
-  static_assert(!(COMPACT && WITH_XY), "compact records carry no screen-position tangent");
-  jvp_tile<WITH_XY, !COMPACT, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec,
+  jvp_tile<WITH_XY, true, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, ranges[tile], point_list, rec,
                                  trec, s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
   if (inside) {
     const int64_t HW = (int64_t)v.H * v.W;

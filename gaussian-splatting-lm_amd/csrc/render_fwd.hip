@@ -1,100 +1,20 @@
 // render_fwd.hip -- the rasterizer forward's per-tile blend (upstream renderCUDA semantics, SURVEY App. A
-// step 11): one 16x16 tile per 256-thread block, wave w on the tile's 8x8 quadrant w (tile_pixel), list
-// entries staged through LDS 256 at a time, each wave visiting only the entries whose alpha region reaches
-// its quadrant (publish_quad_masks), front to back until T < 1e-4.
+// step 11): one 16x16 tile per 256-thread block, wave w on the tile's 8x8 quadrant w (tile_pixel), each wave
+// visiting only the list entries whose alpha region reaches its quadrant (the point list's quadrant masks),
+// front to back until T < 1e-4.
 //
 // Compiled apart from the per-Gaussian kernels with -fno-slp-vectorize (Makefile), like the other tile
 // passes: the loop body is scalar f32 math and one branch, the per-lane stop kept as a lane mask (the wave
-// leaves the batch when every lane has stopped), no software pipelining of the next record.
+// leaves when every lane has stopped), no software pipelining of the next records (measured: no gain).
 #include "gslm_tile.hpp"
 
 namespace gslm {
 
-__global__ __launch_bounds__(256) void k_render_fwd(ViewK v, const uint2* __restrict__ ranges,
-                                                     const uint32_t* __restrict__ tile_order,
-                                                     const uint32_t* __restrict__ point_list,
-                                                     const float4* __restrict__ rec, float* __restrict__ out_color,
-                                                     float* __restrict__ out_invdepth, float* __restrict__ final_T,
-                                                     uint32_t* __restrict__ n_contrib) {
-  __shared__ float4 s_r0[TILE_PIX], s_r1[TILE_PIX];
-  __shared__ float2 s_r2[TILE_PIX];
-  __shared__ uint64_t s_bits[16];
-  __shared__ int s_cnt[4];
-  const int tile = (int)tile_order[blockIdx.x];
-  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
-  const int tid = threadIdx.x, w = tid >> 6;
-  int px, py;
-  tile_pixel(tile_x, tile_y, tid, px, py);
-  const bool inside = px < v.W && py < v.H;
-  const float pxf = (float)px, pyf = (float)py;
-  bool done = !inside;
-  const uint2 range = ranges[tile];
-  const int n = (int)(range.y - range.x);
-  const int rounds = (n + TILE_PIX - 1) / TILE_PIX;
-
-  float T = 1.0f;
-  uint32_t last = 0;
-  float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  for (int r = 0; r < rounds; ++r) {
-    __syncthreads();  // the previous batch is consumed (and block_count's words are free)
-    if (block_count(done, s_cnt) == TILE_PIX) break;
-    const int k = r * TILE_PIX + tid;
-    uint32_t m = 0u;
-    if (k < n) {
-      const uint32_t e = point_list[range.x + k];
-      const int64_t gidx = pl_id(e);
-      m = pl_mask(e);
-      s_r0[tid] = rec[3 * gidx + 0];
-      s_r1[tid] = rec[3 * gidx + 1];
-      const float4 r2 = rec[3 * gidx + 2];
-      s_r2[tid] = make_float2(r2.x, r2.y);
-    }
-    publish_quad_masks(m, s_bits);
-    __syncthreads();
-    if (__ballot(!done) == 0ull) continue;  // every pixel of this quadrant has stopped
-    HitIter it(s_bits, w);
-    for (int j = it.next(); j >= 0; j = it.next()) {
-      const float4 a = s_r0[j], b = s_r1[j];
-      const float2 cc = s_r2[j];
-      // the whole record in one LDS round trip (the colour half would otherwise load inside the branch)
-      asm volatile("" : : "v"(b.z), "v"(b.w), "v"(cc.x), "v"(cc.y));
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-      const float alpha = fminf(0.99f, b.y * gexp(power));
-      const float test_T = T * (1.0f - alpha);
-      if (!done && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-        if (test_T < 0.0001f) {
-          done = true;
-        } else {
-          const float wt = alpha * T;
-          C0 += b.z * wt;
-          C1 += b.w * wt;
-          C2 += cc.x * wt;
-          Dp += cc.y * wt;
-          T = test_T;
-          last = (uint32_t)(r * TILE_PIX + j + 1);  // 1-based list position
-        }
-      }
-      if (__ballot(!done) == 0ull) break;
-    }
-  }
-  if (inside) {
-    const int64_t pid = (int64_t)py * v.W + px;
-    const int64_t HW = (int64_t)v.H * v.W;
-    final_T[pid] = T;
-    n_contrib[pid] = last;
-    out_color[pid] = C0 + T * v.bg[0];
-    out_color[HW + pid] = C1 + T * v.bg[1];
-    out_color[2 * HW + pid] = C2 + T * v.bg[2];
-    if (out_invdepth) out_invdepth[pid] = Dp;
-  }
-}
-
-// The same blend with one independent wave per 8x8 quadrant: 64 list positions per round, each lane fetches
-// one, the entries whose mask holds the quadrant stage their record in the wave's own LDS slots (lane-indexed),
-// and the wave walks the round's hit bits in list order.  No block barrier: a wave leaves as soon as all of
-// its pixels have stopped, however far the tile's other quadrants still go.  Per-lane arithmetic and
-// decisions as k_render_fwd.
+// One independent wave per 8x8 quadrant: 64 list positions per round, each lane fetches one, the entries whose
+// mask holds the quadrant stage their record in the wave's own LDS slots (lane-indexed), and the wave walks the
+// round's hit bits in list order.  No block barrier: a wave leaves as soon as all of its pixels have stopped,
+// however far the tile's other quadrants still go (a block-cooperative version with 256-entry LDS batches
+// measured 1.5% slower on the full forward).
 __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* __restrict__ ranges,
                                                           const uint32_t* __restrict__ tile_order,
                                                           const uint32_t* __restrict__ point_list,
