@@ -194,7 +194,7 @@ class GaussianShardedOperator:
     Per product (matvec_dot), with b = (k, t) running over every view (k-th view of rank t):
       1. gslm_tangent_views: this shard's tangent render records for every view (the fused direction
          update p = s + beta p [, x += alpha p] on the shard first) -> trec[k][t][S][8];
-      2. all_to_all per k: rank t receives every shard's records of its k-th view = a [P][12] table;
+      2. all_to_all per k: rank t receives every shard's records of its k-th view = a [P][8] table;
       3. RENDER | SCREEN with opts.trec_in: the view's fused JVP -> VJP tile pass and row sums -> [P][8];
       4. all_to_all per k: rank r receives the [S][8] slices of its shard from every view;
       5. gslm_gather_screen over the shard, every view's chain, + D v, <v, y> partial.
@@ -213,6 +213,7 @@ class GaussianShardedOperator:
         self.local = local
         self.group = group
         self.rank, self.world_size = world()
+        self._slot_index = {}  # allreduce_scalars' device index tensors, per slot tuple
         full = local.layout
         if getattr(full, "rest_projected", False):
             raise ValueError("the Gaussian-sharded exchange runs on the full SH-rest layout")
@@ -256,10 +257,18 @@ class GaussianShardedOperator:
         _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
 
     def allreduce_scalars(self, sc, slots):
-        """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks."""
+        """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks.  One slot (the CG
+        loop's delta and gamma' without the residual monitor): in place on the 8-byte view, no gather / scatter
+        kernels and no host-to-device index copy around the collective."""
         if self.world_size == 1:
             return
-        idx = torch.tensor(list(slots), device=sc.device)
+        slots = tuple(slots)
+        if len(slots) == 1:
+            self._allreduce(sc[slots[0]:slots[0] + 1])
+            return
+        idx = self._slot_index.get(slots)
+        if idx is None:
+            idx = self._slot_index[slots] = torch.tensor(slots, device=sc.device)
         t = sc.index_select(0, idx)
         self._allreduce(t)
         sc.index_copy_(0, idx, t)
