@@ -154,11 +154,9 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
   if (k == N - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
 }
 
-// Gradient-row slot of every sorted entry (row_slot), so the tile passes read it coalesced instead
-// of gathering goff / rect per entry.  The goff / rect gathers here are random over 12 B/Gaussian
-// (~90 us at 1M Gaussians / 4.9M entries), so the fused LM product computes the slots once per
-// geometry (GSLM_MV_TAIL_CLEAN protocol) and the forward does not.
 // ---- the LM row map (ScratchBufs::hscan), once per geometry ----
+// Computed by the first LM product on a geometry (GSLM_MV_TAIL_CLEAN protocol), not by the forward: the
+// goff / rect gathers are random over 12 B per Gaussian and the drop-in backward does not need the map.
 // largest n_contrib over each tile's pixels: list positions at or past it are blended by no pixel of the tile
 __global__ __launch_bounds__(256) void k_tile_neff(ViewK v, const uint32_t* __restrict__ n_contrib,
                                                     uint32_t* __restrict__ neff) {
