@@ -51,12 +51,14 @@ def main(out_dir):
                                   "python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --forward-steps 8",
                        "fetch_bytes_per_launch_raw": r["fetch_bytes_per_launch_raw"],
                        "write_bytes_per_launch": r["write_bytes_per_launch"],
-                       "hbm_bytes_per_launch": r["fetch_bytes_per_launch_raw"] + r["write_bytes_per_launch"],
-                       "hbm_bytes_per_launch_if_x2": r["fetch_bytes_per_launch_x2"] + r["write_bytes_per_launch"],
-                       "correction_note": "FETCH_SIZE/WRITE_SIZE are KiB per dispatch. The gfx950 x2 FETCH "
-                       "correction (MI355X_MICROARCH.md HBM) is calibrated for wide coalesced streams (checked "
-                       "on k_cg_update: 4 x 236 MB read, FETCH reports half); this kernel's reads are 16-B "
-                       "record gathers, so the raw value is reported and the x2 figure is an upper bound."},
+                       "hbm_bytes_per_launch": r["fetch_bytes_per_launch_x2"] + r["write_bytes_per_launch"],
+                       "hbm_bytes_per_launch_raw": r["fetch_bytes_per_launch_raw"] + r["write_bytes_per_launch"],
+                       "correction_note": "FETCH_SIZE / WRITE_SIZE are KiB per dispatch. FETCH_SIZE is doubled: "
+                       "profiles/r02/pmc_calibration.json (tools/pmc_calib.hip, 1 GiB table) measures FETCH at "
+                       "0.50 x the bytes of 16-B and 4-B coalesced streams and at 1.38 x the 48 B of a random "
+                       "48-B record alone in its 128-B line (= half of the whole line the read pulls), so the "
+                       "counter tallies memory-side 128-B line reads at 64 B for this kernel's record gathers "
+                       "too; WRITE_SIZE is exact for 16-B coalesced stores and random 32-B rows (1.00)."},
                       f, indent=1)
 
 
