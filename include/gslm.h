@@ -246,11 +246,11 @@ int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussi
  * Rank r owns Gaussians [r S, (r + 1) S) of every CG vector and the vector algebra on them.  Per product:
  *   gslm_tangent_views   this shard's tangent render records for EVERY view b (chain_jvp, the TANGENT stage
  *                        of gslm_matvec_view_ex for a Gaussian range) -> all-to-all -> each rank holds its
- *                        own view's [P][12] table for opts->trec_in;
+ *                        own view's [P][8] table (mask_xyz; [P][12] without) for opts->trec_in;
  *   RENDER | SCREEN      with opts->trec_in -> [P][8] screen sums -> all-to-all -> each rank holds
  *                        screen[b][S][8] of its shard for every view;
  *   gslm_gather_screen   over the shard (g = the shard's slice of the leaves, opts->screen_stride = S).
- * A rank receives (48 + 32) (n - 1) / n bytes per Gaussian per view it renders instead of the screen
+ * A rank receives (32 + 32) (n - 1) / n bytes per Gaussian per view it renders instead of the screen
  * all-gather's 32 (n - 1), and runs 1/n of the chains and vector algebra.
  * gslm_view_flags: out[i] = 0 if Gaussian i touches no tile of the preprocessed view, else
  * 0x80000000 | its 3 SH-clamp bits (the flags word of the SCREEN rows); exchanged once per geometry. */
