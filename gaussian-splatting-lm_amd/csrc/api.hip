@@ -26,7 +26,7 @@ struct Carver {
 size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
   Carver c{(char*)base};
   GeomBufs g;
-  g.rec = c.take<float4>((size_t)P * REC_F4);
+  g.rec = c.take<float4>((size_t)P * RECS);
   g.depth_key = c.take<uint32_t>(P);
   g.tiles = c.take<uint32_t>(P);
   g.rect = c.take<uint2>(P);
@@ -573,7 +573,8 @@ int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t N, in
   if (tiles_touched && P) GSLM_HIP_CHECK(hipMemcpyAsync(tiles_touched, gb.tiles, (size_t)P * 4, D2D, s));
   if (final_T && image) GSLM_HIP_CHECK(hipMemcpyAsync(final_T, ib.final_T, (size_t)H * W * 4, D2D, s));
   if (n_contrib && image) GSLM_HIP_CHECK(hipMemcpyAsync(n_contrib, ib.n_contrib, (size_t)H * W * 4, D2D, s));
-  if (records && P) GSLM_HIP_CHECK(hipMemcpyAsync(records, gb.rec, (size_t)P * 48, D2D, s));
+  if (records && P)  // 12 floats per Gaussian out of the 64-B record stride
+    GSLM_HIP_CHECK(hipMemcpy2DAsync(records, 48, gb.rec, RECS * sizeof(float4), 48, (size_t)P, D2D, s));
   return GSLM_OK;
 }
 

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* 
   const uint32_t h0 = i < P ? hscan[goff[i]] : R1, h1 = i < P ? hscan[goff[i] + n] : R1;
   block_sum_rows<2>(rows, R0, R1, h0, h1 - h0, s_buf, G2);
   if (i >= P) return;
-  const uint32_t flags = n ? (0x80000000u | (__float_as_uint(rec[3 * i + 2].z) & 7u)) : 0u;
+  const uint32_t flags = n ? (0x80000000u | (__float_as_uint(rec[RECS * i + 2].z) & 7u)) : 0u;
   out[2 * i + 0] = make_float4(G2[2], G2[3], G2[4], G2[5]);
   out[2 * i + 1] = make_float4(G2[6], G2[7], G2[8], __uint_as_float(flags));
 }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_view_flags(int64_t P, const float4* __r
                                                      const uint32_t* __restrict__ tiles, uint32_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
-  out[i] = tiles[i] ? (0x80000000u | (__float_as_uint(rec[3 * i + 2].z) & 7u)) : 0u;
+  out[i] = tiles[i] ? (0x80000000u | (__float_as_uint(rec[RECS * i + 2].z) & 7u)) : 0u;
 }
 
 int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s) {

@@ -1,7 +1,7 @@
 // forward.hip -- rasterizer forward for gfx950.
 //
 //   k_preprocess   one thread per Gaussian: cull, project, cov3D, EWA cov2D, conic, radius,
-//                  rect, SH->RGB; writes a 48-B render record + depth key + tile count.
+//                  rect, SH->RGB; writes a 48-B render record (64-B stride) + depth key + tile count.
 //   (depth sort of P keys + scan of tile counts in depth order: sort.hip)
 //   k_duplicate    emits (tile id, Gaussian id) pairs in depth order: the later *stable* sort on
 //                  the tile id alone then yields upstream's (tile, depth, index) order with
@@ -46,9 +46,9 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
   const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
   const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.tq);
-  rec[3 * i + 0] = r0;
-  rec[3 * i + 1] = r1;
-  rec[3 * i + 2] = r2;
+  rec[RECS * i + 0] = r0;
+  rec[RECS * i + 1] = r1;
+  rec[RECS * i + 2] = r2;
   depth_key[i] = __float_as_uint(o.depth);
   tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
   rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
@@ -84,8 +84,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
       s_rc[tid][1] = (uint32_t)y0;
       s_rc[tid][2] = (uint32_t)(x1 - x0);
       s_g[tid] = g;
-      const float4 r0 = rec[3 * (int64_t)g + 0];
-      s_q[tid] = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, rec[3 * (int64_t)g + 1].x, rec[3 * (int64_t)g + 2].w);
+      const float4 r0 = rec[RECS * (int64_t)g + 0];
+      s_q[tid] = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, rec[RECS * (int64_t)g + 1].x, rec[RECS * (int64_t)g + 2].w);
     }
   } else {
     s_off[tid] = 0xFFFFFFFFu;  // past the block's last Gaussian: never an owner

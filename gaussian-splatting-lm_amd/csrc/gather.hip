@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
   const bool sh_out = !g.colors && (out.dc || out.rest);
   ChainOut co;
   if (i < g.P) {
-    chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, want_means != 0, co);
+    chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[RECS * i + 2].z) : 0u, G2, want_means != 0, co);
     write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
   }
   if (!sh_out) return;  // block-uniform
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK
     block_sum_rows<ROWF4>(rows, R0, R1, h0, h1 - h0, reinterpret_cast<float4*>(s_rest), G2);
   }
   ChainOut co;
-  if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[3 * i + 2].z) : 0u, G2, WANT_MEANS, co);
+  if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[RECS * i + 2].z) : 0u, G2, WANT_MEANS, co);
   lm_epilogue<WANT_MEANS, true>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
 }
 

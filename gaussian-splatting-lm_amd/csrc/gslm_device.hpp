@@ -14,7 +14,10 @@ namespace gslm {
 constexpr int TILE_X = 16;
 constexpr int TILE_Y = 16;
 constexpr int TILE_PIX = TILE_X * TILE_Y;  // 256 threads = 4 wave64 per tile
-constexpr int REC_F4 = 3;                  // render record = 3 float4 (48 B) per Gaussian
+constexpr int REC_F4 = 3;                  // 3 float4 (48 B): drop-in tangent records and gradient rows
+// Render records [x y a b | c o r g | b 1/z clampbits z] (48 B) at a 64-B stride: a record never straddles a
+// 128-B line, so each gather of one by the tile passes pulls a single line.
+constexpr int RECS = 4;
 
 // utils/sh_utils.py:26-55
 __constant__ static const float SH_C0 = 0.28209479177387814f;

@@ -222,9 +222,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       const uint32_t e = point_list[range.x + base - tid];
       const uint32_t g = pl_id(e);
       my_mask = pl_mask(e);
-      s_r0[tid] = rec[3 * (int64_t)g + 0];
-      s_r1[tid] = rec[3 * (int64_t)g + 1];
-      const float4 r2 = rec[3 * (int64_t)g + 2];
+      s_r0[tid] = rec[RECS * (int64_t)g + 0];
+      s_r1[tid] = rec[RECS * (int64_t)g + 1];
+      const float4 r2 = rec[RECS * (int64_t)g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
       my_slot = slots ? slots[range.x + base - tid] : row_slot(goff[g], rect[g], tile_x, tile_y);
       // and only the waves that still blend at this list position

@@ -52,9 +52,9 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
       const int64_t g = pl_id(e);
       // quadrants it can touch, and only the waves that still blend at this list position
       m = pl_mask(e) & ((k < wm0 ? 1u : 0u) | (k < wm1 ? 2u : 0u) | (k < wm2 ? 4u : 0u) | (k < wm3 ? 8u : 0u));
-      s_r0[tid] = rec[3 * g + 0];
-      s_r1[tid] = rec[3 * g + 1];
-      const float4 r2 = rec[3 * g + 2];
+      s_r0[tid] = rec[RECS * g + 0];
+      s_r1[tid] = rec[RECS * g + 1];
+      const float4 r2 = rec[RECS * g + 2];
       if (PACKED) {
         // the LM rows' compact tangent record (store_trec): [da db dc dop | dr dg db 0].  The product's 9 primal +
         // 7 tangent floats as 4 float4 at one LDS stride: the hit loop reads them with one address register;
@@ -163,7 +163,7 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
       if ((pl_mask(e) >> q) & 1u) {
         hit = true;
         const uint32_t g = pl_id(e);
-        const float4 r0 = rec[3 * (size_t)g + 0], r1 = rec[3 * (size_t)g + 1], r2 = rec[3 * (size_t)g + 2];
+        const float4 r0 = rec[RECS * (size_t)g + 0], r1 = rec[RECS * (size_t)g + 1], r2 = rec[RECS * (size_t)g + 2];
         const float4 c0 = trec[2 * (size_t)g + 0], c1 = trec[2 * (size_t)g + 1];
         s[lane] = r0;
         s[64 + lane] = r1;

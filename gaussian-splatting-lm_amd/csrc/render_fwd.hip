@@ -47,9 +47,9 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       if ((pl_mask(e) >> q) & 1u) {
         hit = true;
         const uint32_t g = pl_id(e);
-        s[lane] = rec[3 * (size_t)g + 0];
-        s[64 + lane] = rec[3 * (size_t)g + 1];
-        s[128 + lane] = rec[3 * (size_t)g + 2];
+        s[lane] = rec[RECS * (size_t)g + 0];
+        s[64 + lane] = rec[RECS * (size_t)g + 1];
+        s[128 + lane] = rec[RECS * (size_t)g + 2];
       }
     }
     uint64_t hb = __ballot(hit);

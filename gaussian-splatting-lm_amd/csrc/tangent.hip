@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
   if (i >= g.P) return;
   if (tiles[i] == 0) return;  // never gathered by the render passes
   float T2[10];
-  chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[3 * i + 2].z), T2);
+  chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[RECS * i + 2].z), T2);
   store_trec(trec, i, T2, compact != 0);
 }
 
