@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--stagger", type=int, nargs="*", default=[],
                     help="also time the gather with its output vector offset by K floats (HBM channel alignment)")
     ap.add_argument("--ramp", type=int, default=0, help="also time N single CG iterations back to back (clock ramp)")
+    ap.add_argument("--cg-scan", type=int, nargs="*", default=[],
+                    help="also time cgls_fused calls of K iterations: wall clock per iteration and the host's enqueue time")
     a = ap.parse_args()
     if a.compare:
         compare(a.compare[0], a.compare[1:])
@@ -136,6 +138,16 @@ def main():
     cgls_fused(prob, g, max_iter=a.reps, restart_iter=a.reps, check_every=False)
     torch.cuda.synchronize()
     res["cg_iter_ms"] = 1e3 * (time.perf_counter() - t0) / a.reps
+    for k in a.cg_scan:
+        cgls_fused(prob, g, max_iter=3, restart_iter=3, check_every=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cgls_fused(prob, g, max_iter=k, restart_iter=k, check_every=False)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        res[f"cg{k}_iter_ms"] = round(1e3 * (t2 - t0) / k, 4)
+        res[f"cg{k}_enqueue_ms_per_iter"] = round(1e3 * (t1 - t0) / k, 4)
     if a.ramp:
         # per-iteration device time of N consecutive CG iterations, launched without host syncs
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.ramp)]
