@@ -220,14 +220,16 @@ class GaussianRasterizer(nn.Module):
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
                 cov3D_precomp=None, dc=None):
-        shs, colors_precomp = _none_if_empty(shs), _none_if_empty(colors_precomp)
-        scales, rotations, cov3D_precomp = _none_if_empty(scales), _none_if_empty(rotations), _none_if_empty(cov3D_precomp)
-        dc = _none_if_empty(dc)
-        has_sh = shs is not None or dc is not None  # separate_sh at SH degree 0: dc= with an empty rest
+        # upstream's exactly-one checks look at None, not at emptiness (an empty SH rest at degree 0 with dc=, or
+        # every tensor of a P = 0 model, is a given argument); empty tensors become "absent" only afterwards
+        has_sh = shs is not None or dc is not None
         if (not has_sh and colors_precomp is None) or (has_sh and colors_precomp is not None):
             raise Exception("Please provide excatly one of either SHs or precomputed colors!")
         if ((scales is None or rotations is None) and cov3D_precomp is None) or (
                 (scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        shs, colors_precomp = _none_if_empty(shs), _none_if_empty(colors_precomp)
+        scales, rotations, cov3D_precomp = _none_if_empty(scales), _none_if_empty(rotations), _none_if_empty(cov3D_precomp)
+        dc = _none_if_empty(dc)
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations,
                                    cov3D_precomp, self.raster_settings, dc=dc)

@@ -87,6 +87,12 @@ def test_rasterizer_argument_validation():
         r(means3D=x, means2D=x, opacities=torch.zeros(4, 1), scales=x, rotations=torch.zeros(4, 4))
     with pytest.raises(Exception, match="scale/rotation pair"):
         r(means3D=x, means2D=x, opacities=torch.zeros(4, 1), colors_precomp=x)
+    # upstream's checks test for None, not emptiness: an empty colors_precomp beside shs is a second colour
+    # source (raises), while an empty SH rest beside dc= (separate_sh at degree 0) or the empty tensors of a
+    # P = 0 model are given arguments (tests/test_gpu_edge.py renders those)
+    with pytest.raises(Exception, match="one of either SHs or precomputed colors"):
+        r(means3D=x, means2D=x, opacities=torch.zeros(4, 1), shs=torch.zeros(4, 1, 3), colors_precomp=torch.zeros(0),
+          scales=x, rotations=torch.zeros(4, 4))
 
 
 def test_simple_knn_module_binds_the_hip_kernel():
