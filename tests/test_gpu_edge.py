@@ -191,3 +191,39 @@ def test_lm_product_nothing_visible():
             lo, hi = prob.layout.offsets[name]
             dv[lo:hi] = float(d) * v[lo:hi]
     assert torch.allclose(y, dv, rtol=0, atol=0), float((y - dv).abs().max())
+
+
+@pytest.mark.parametrize("max_deg,active,W,H", [(0, 0, 40, 33), (1, 1, 64, 48), (2, 2, 17, 23), (3, 1, 48, 40)])
+@pytest.mark.parametrize("projected", [False, True])
+def test_lm_product_sh_degrees_and_sizes(max_deg, active, W, H, projected):
+    """The LM loss, J^T b and (J^T J + D) v against the oracle's operator for SH degrees 0-2, an active degree
+    below the stored one (train_jvp.py's progressive oneupSHdegree), ragged images, and the single-view
+    projected SH-rest layout where it applies (1e-4 of the vector's max, loss rel 1e-5)."""
+    import copy
+    from gslm.lm import LMProblem
+    from oracle.lm_ref import OracleLMProblem
+    model = _model(1500, max_deg, 0.04, seed=11)
+    model.active_sh_degree = active
+    cam = _cam(W, H, seed=4)
+    cam.original_image = torch.rand(3, H, W, generator=torch.Generator().manual_seed(8))
+    mc, cc = copy.deepcopy(model), copy.deepcopy(cam)
+    op = OracleLMProblem(mc, [cc], torch.zeros(3))
+    lo = float(op.evaluate())
+    prob = LMProblem(model.to(DEV), [cam.to(DEV)], torch.zeros(3), device=DEV, sh_projection=projected)
+    assert prob.layout.rest_projected == (projected and max_deg > 0)
+    assert abs(float(prob.evaluate()) - lo) <= 1e-5 * lo
+    assert prob.num_rendered()[0] > 1000
+    g = prob.rhs(prob.zeros())
+    go = op.rhs()
+    full = prob.expand(g).cpu() if prob.layout.rest_projected else g.cpu()
+    assert _rel_err(full, go) < 1e-4, _rel_err(full, go)
+    v = torch.randn(prob.layout.numel, generator=torch.Generator().manual_seed(9)).to(DEV)
+    for name in ("xyz", "exposure"):
+        a, b = prob.layout.offsets[name]
+        v[a:b] = 0
+    y = prob.matvec(v, prob.zeros())
+    vf = prob.expand(v) if prob.layout.rest_projected else v
+    yo = op.zeros()
+    op.matvec(vf.cpu(), yo)
+    yf = prob.expand(y).cpu() if prob.layout.rest_projected else y.cpu()
+    assert _rel_err(yf, yo) < 1e-4, _rel_err(yf, yo)
