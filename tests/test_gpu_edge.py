@@ -227,3 +227,32 @@ def test_lm_product_sh_degrees_and_sizes(max_deg, active, W, H, projected):
     op.matvec(vf.cpu(), yo)
     yf = prob.expand(y).cpu() if prob.layout.rest_projected else y.cpu()
     assert _rel_err(yf, yo) < 1e-4, _rel_err(yf, yo)
+
+
+@pytest.mark.parametrize("W,H", [(5, 7), (17, 23), (40, 33)])
+def test_lm_ssim_product_small_and_ragged_images(W, H):
+    """The SSIM residual's loss, J^T b and (J^T J + D) v (batch_training_loss.py:18-30) against the oracle on
+    images smaller than the 11-tap window and on ragged sizes (the separable window's border handling)."""
+    import copy
+    from gslm.lm import LMProblem
+    from oracle.lm_ref import OracleLMProblem
+    model = _model(800, 2, 0.05, seed=12)
+    cam = _cam(W, H, seed=6)
+    cam.original_image = torch.rand(3, H, W, generator=torch.Generator().manual_seed(10))
+    mc, cc = copy.deepcopy(model), copy.deepcopy(cam)
+    op = OracleLMProblem(mc, [cc], torch.zeros(3), ssim=True)
+    lo = float(op.evaluate())
+    prob = LMProblem(model.to(DEV), [cam.to(DEV)], torch.zeros(3), device=DEV, ssim=True, sh_projection=False)
+    assert abs(float(prob.evaluate()) - lo) <= 1e-5 * lo
+    assert prob.num_rendered()[0] > 0
+    g = prob.rhs(prob.zeros())
+    go = op.rhs()
+    assert _rel_err(g.cpu(), go) < 1e-4, _rel_err(g.cpu(), go)
+    v = torch.randn(prob.layout.numel, generator=torch.Generator().manual_seed(9)).to(DEV)
+    for name in ("xyz", "exposure"):
+        a, b = prob.layout.offsets[name]
+        v[a:b] = 0
+    y = prob.matvec(v, prob.zeros())
+    yo = op.zeros()
+    op.matvec(v.cpu(), yo)
+    assert _rel_err(y.cpu(), yo) < 1e-4, _rel_err(y.cpu(), yo)
