@@ -39,6 +39,7 @@ size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
   g.hist = c.take<uint32_t>(sort_hist_bytes(P) / 4);
   g.scan_tmp = c.take<uint32_t>(scan_tmp_bytes(P) / 4);
   g.counters = c.take<uint32_t>(16);
+  g.clampw = c.take<uint32_t>(P);
   if (o) *o = g;
   return c.off;
 }

@@ -15,7 +15,7 @@
 
 namespace gslm {
 
-__global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* __restrict__ rec,
+__global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const uint32_t* __restrict__ clampw,
                                                         const uint32_t* __restrict__ tiles,
                                                         const uint32_t* __restrict__ goff,
                                                         const uint32_t* __restrict__ hscan,
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const float4* 
   const uint32_t h0 = i < P ? hscan[goff[i]] : R1, h1 = i < P ? hscan[goff[i] + n] : R1;
   block_sum_rows<2>(rows, R0, R1, h0, h1 - h0, s_buf, G2);
   if (i >= P) return;
-  const uint32_t flags = n ? (0x80000000u | (__float_as_uint(rec[RECS * i + 2].z) & 7u)) : 0u;
+  const uint32_t flags = n ? (0x80000000u | (clampw[i] & 7u)) : 0u;
   out[2 * i + 0] = make_float4(G2[2], G2[3], G2[4], G2[5]);
   out[2 * i + 1] = make_float4(G2[6], G2[7], G2[8], __uint_as_float(flags));
 }
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, cons
 
 int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_rowsum_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, g.P, gb.rec, gb.tiles,
+  hipLaunchKernelGGL(k_rowsum_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, g.P, gb.clampw, gb.tiles,
                      gb.goff, sb.hscan, sb.contrib, reinterpret_cast<float4*>(out));
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
@@ -107,16 +107,16 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
 
 // Visibility / SH-clamp word of every Gaussian of a preprocessed view (the SCREEN rows' flags), for
 // the Gaussian-sharded exchange's once-per-geometry all-to-all.
-__global__ __launch_bounds__(256) void k_view_flags(int64_t P, const float4* __restrict__ rec,
+__global__ __launch_bounds__(256) void k_view_flags(int64_t P, const uint32_t* __restrict__ clampw,
                                                      const uint32_t* __restrict__ tiles, uint32_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
-  out[i] = tiles[i] ? (0x80000000u | (__float_as_uint(rec[RECS * i + 2].z) & 7u)) : 0u;
+  out[i] = tiles[i] ? (0x80000000u | (clampw[i] & 7u)) : 0u;
 }
 
 int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s) {
   if (P == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, gb.rec, gb.tiles, out);
+  hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, gb.clampw, gb.tiles, out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -21,7 +21,7 @@ template <bool RAW, bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* __restrict__ rec,
                                                      uint32_t* __restrict__ depth_key,
                                                      uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
-                                                     int* __restrict__ radii_out) {
+                                                     uint32_t* __restrict__ clampw, int* __restrict__ radii_out) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];  // STAGE: [256 * rest_stride]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (STAGE) {
@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   depth_key[i] = __float_as_uint(o.depth);
   tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
   rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  clampw[i] = o.clamped;  // read only where tiles[i] != 0
   if (radii_out) radii_out[i] = o.radius;
 }
 
@@ -223,16 +224,16 @@ int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* 
   const size_t lds = stage ? (size_t)256 * g.rest_stride * sizeof(float) : 0;
   if (g.raw && stage)
     hipLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, radii_out);
+                       gb.rect, gb.clampw, radii_out);
   else if (g.raw)
     hipLaunchKernelGGL((k_preprocess<true, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, radii_out);
+                       gb.rect, gb.clampw, radii_out);
   else if (stage)
     hipLaunchKernelGGL((k_preprocess<false, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, radii_out);
+                       gb.rect, gb.clampw, radii_out);
   else
     hipLaunchKernelGGL((k_preprocess<false, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, radii_out);
+                       gb.rect, gb.clampw, radii_out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -32,7 +32,7 @@ __device__ __forceinline__ void sum_rows(const float4* __restrict__ rows, uint32
 // the bulk of the output -- staged through LDS and stored as contiguous wave segments (per-thread
 // stores at a 3M-float stride would touch a cache line per lane per store).
 template <bool RAW>
-__global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const float4* __restrict__ rec,
+__global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const uint32_t* __restrict__ clampw,
                                                          const uint32_t* __restrict__ tiles,
                                                          const uint32_t* __restrict__ goff,
                                                          const float4* __restrict__ rows, GradK out, int want_means) {
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
   const bool sh_out = !g.colors && (out.dc || out.rest);
   ChainOut co;
   if (i < g.P) {
-    chain_vjp<RAW>(v, g, i, n != 0, n ? __float_as_uint(rec[RECS * i + 2].z) : 0u, G2, want_means != 0, co);
+    chain_vjp<RAW>(v, g, i, n != 0, n ? clampw[i] : 0u, G2, want_means != 0, co);
     write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
   }
   if (!sh_out) return;  // block-uniform
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
 // vector groups).  The full-layout variant keeps the compiler's register count: forced to 96 VGPRs its SH-rest
 // epilogue spills and takes 0.18 -> 0.31 ms.
 template <bool WANT_MEANS, int ROWF4, bool PROJ>
-__global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK g, const float4* __restrict__ rec,
+__global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK g, const uint32_t* __restrict__ clampw,
                                                     const uint32_t* __restrict__ tiles,
                                                     const uint32_t* __restrict__ goff,
                                                     const uint32_t* __restrict__ hscan,
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK
     block_sum_rows<ROWF4>(rows, R0, R1, h0, h1 - h0, reinterpret_cast<float4*>(s_rest), G2);
   }
   ChainOut co;
-  if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? __float_as_uint(rec[RECS * i + 2].z) : 0u, G2, WANT_MEANS, co);
+  if (i < g.P) chain_vjp<true>(v, g, i, n != 0, n ? clampw[i] : 0u, G2, WANT_MEANS, co);
   lm_epilogue<WANT_MEANS, true>((v.D + 1) * (v.D + 1), g, co, o, s_rest, s_dot);
 }
 
@@ -187,10 +187,10 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
   const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
   const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
   if (g.raw)
-    hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.contrib, out, want_means ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.contrib, out, want_means ? 1 : 0);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
@@ -208,16 +208,16 @@ int launch_gather_lm(const ViewK& v, const GaussK& g, const GeomBufs& gb, const 
   const size_t chunk_lds = (size_t)GATHER_CHUNK * (mask_xyz ? 2 : 3) * sizeof(float4);
   const size_t lds = (rest_lds > chunk_lds ? rest_lds : chunk_lds) + 16;
   if (mask_xyz && o.rest_proj)
-    hipLaunchKernelGGL((k_gather_lm<false, 2, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL((k_gather_lm<false, 2, true>), dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   else if (mask_xyz)
-    hipLaunchKernelGGL((k_gather_lm<false, 2, false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL((k_gather_lm<false, 2, false>), dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   else if (o.rest_proj)
-    hipLaunchKernelGGL((k_gather_lm<true, 3, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL((k_gather_lm<true, 3, true>), dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   else
-    hipLaunchKernelGGL((k_gather_lm<true, 3, false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.tiles, gb.goff,
+    hipLaunchKernelGGL((k_gather_lm<true, 3, false>), dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,
                        sb.hscan, sb.contrib, o);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

@@ -322,6 +322,8 @@ struct GeomBufs {
   uint32_t* hist;         // radix histogram
   uint32_t* scan_tmp;     // scan block sums
   uint32_t* counters;     // [0] = num_rendered, [1] = sum of tiles (== [0])
+  uint32_t* clampw;       // [P] SH clamp bits of each visible Gaussian's colour (rec r2.z), read coalesced by the
+                          //     per-Gaussian passes instead of a 64-B record line each
 };
 // Binning: (tile id, Gaussian id) pairs emitted in depth order, stably sorted by tile id.
 // The number of radix passes (hence which ping-pong buffer holds the result) depends only on the

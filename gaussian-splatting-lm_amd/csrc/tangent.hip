@@ -103,7 +103,7 @@ __device__ __forceinline__ void store_trec(float4* __restrict__ out, int64_t i, 
 
 template <bool RAW, bool XPBY>
 __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
-                                                         const float4* __restrict__ rec,
+                                                         const uint32_t* __restrict__ clampw,
                                                          const uint32_t* __restrict__ tiles,
                                                          float4* __restrict__ trec, XpbyK xp, int compact) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
   if (i >= g.P) return;
   if (tiles[i] == 0) return;  // never gathered by the render passes
   float T2[10];
-  chain_jvp<RAW>(v, g, t, m2t, i, __float_as_uint(rec[RECS * i + 2].z), T2);
+  chain_jvp<RAW>(v, g, t, m2t, i, clampw[i], T2);
   store_trec(trec, i, T2, compact != 0);
 }
 
@@ -141,17 +141,17 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
     }
     const size_t lds = (size_t)256 * xp->w[2] * sizeof(float);
     if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
                          sb.trec, x, compact ? 1 : 0);
     else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
                          sb.trec, x, compact ? 1 : 0);
   } else {
     if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.clampw, gb.tiles,
                          sb.trec, x, compact ? 1 : 0);
     else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.rec, gb.tiles,
+      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.clampw, gb.tiles,
                          sb.trec, x, compact ? 1 : 0);
   }
   GSLM_LAUNCH_CHECK();
