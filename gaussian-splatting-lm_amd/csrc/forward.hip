@@ -61,8 +61,7 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
 // spread over the block instead of one thread's loop).  Element e belongs to the last Gaussian whose
 // local offset is <= e (binary search in LDS); inside a Gaussian the rect is walked row-major.
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
-                                                    const uint32_t* __restrict__ offsets,
-                                                    const uint32_t* __restrict__ tiles,
+                                                    const uint32_t* __restrict__ offsets, uint32_t N,
                                                     const uint2* __restrict__ rect, const float4* __restrict__ rec,
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   __shared__ QuadCull s_q[256];
@@ -76,8 +75,11 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   uint32_t n = 0;
   if (s < P) {
     const uint32_t g = sorted_idx[s];
-    n = tiles[g];
-    s_off[tid] = offsets[s] - base;
+    // the tile count from the depth-order scan (coalesced) instead of tiles[g] (a random line per Gaussian);
+    // culled Gaussians (n = 0) then touch nothing else
+    const uint32_t o = offsets[s];
+    n = (s + 1 < P ? offsets[s + 1] : N) - o;
+    s_off[tid] = o - base;
     if (n) {
       const uint2 rc = rect[g];
       const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
@@ -243,7 +245,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0)
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
-                       gb.offsets, gb.tiles, gb.rect, gb.rec, bb.keys0, bb.vals0);
+                       gb.offsets, (uint32_t)N, gb.rect, gb.rec, bb.keys0, bb.vals0);
   GSLM_LAUNCH_CHECK();
   if (N == 0) {  // every range stays [0, 0); the tile passes still read a launch order
     hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
