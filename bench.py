@@ -322,9 +322,10 @@ def main():
         c0 = cpu_config0_times(repeats=5, threads=threads)
         cpu = {"value": 1.0 / r["matvec_s"], "unit": "view-matvec/s", "cores": r["threads"], "kind": "port",
                "sample": (f"oracle/torch_raster.py (PyTorch CPU, {r['threads']} threads, {r['cpu_model']}): "
-                          f"all {args.P} Gaussians through preprocess+binning with forward-AD and autograd, "
-                          f"blend JVP+VJP on {r['n_tiles']} of {r['ntiles']} tiles spread over the 1080p frame, "
-                          f"scaled to the full frame (median of 3); t_pre={r['t_pre']:.2f}s t_sub={r['t_sub']:.2f}s"),
+                          f"all {args.P} Gaussians through preprocess+binning with forward-AD and autograd "
+                          f"(t_gauss={r['t_gauss']:.2f}s, timed whole), blend JVP+VJP on {r['n_tiles']} of "
+                          f"{r['ntiles']} tiles spread over the 1080p frame (t_tiles={r['t_tiles']:.3f}s, timed on "
+                          f"their own) scaled by {r['ntiles']}/{r['n_tiles']}; each phase the median of 3"),
                "raster_mpix_s": W * H / r["forward_s"] / 1e6,
                "host": host_info(),
                "threads_note": "OMP_NUM_THREADS threads (the GPU box's CPU share for this job; os.cpu_count() "

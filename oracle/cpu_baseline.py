@@ -4,9 +4,10 @@ Times the CPU restatement (oracle/torch_raster.py, PyTorch on the host cores) on
 of the benchmark workload and scales it to the full frame:
 
   * the per-Gaussian stages (activations, preprocess, binning, and their forward-AD / autograd
-    passes) run on ALL P Gaussians -- measured once with an empty tile set (t_pre);
-  * the per-tile blend (forward, JVP, VJP) runs on `n_tiles` tiles spread uniformly over the
-    frame (t_sub); the full-frame time is t_pre + (t_sub - t_pre) * ntiles / n_tiles.
+    passes) run on ALL P Gaussians and are timed as they are (t_gauss);
+  * the per-tile blend (forward-AD, autograd forward + backward to the screen-space tensors) runs
+    on `n_tiles` tiles spread uniformly over the frame and is timed on its own (t_tiles); the
+    full-frame time is t_gauss + t_tiles * ntiles / n_tiles.
 
 One "matvec" here is the reference's J v (torch forward-AD, solver_functions.py:83-99) plus
 J^T u (autograd backward, solver_functions.py:101-132) of one view -- the CPU analogue of one
@@ -22,69 +23,96 @@ import torch.autograd.forward_ad as fwAD
 from oracle import torch_raster as tr
 
 
-def _render_subset(model, cam, bg, subset, means2D=None):
-    st = tr.settings_from_camera(cam, bg, model.active_sh_degree)
-    m2 = torch.zeros_like(model.get_xyz) if means2D is None else means2D
+_SCREEN = ("xy", "conic", "opacity", "rgb")
+
+
+def _preprocess_binning(model, st):
+    m2 = torch.zeros_like(model.get_xyz)
     pre = tr.preprocess(model.get_xyz, m2, model.get_opacity, model.get_features, None, model.get_scaling,
                         model.get_rotation, None, st)
     pl, _, ranges = tr.binning(pre)
-    color, _, _, _ = tr.blend(pre, pl, ranges, st.image_height, st.image_width, st.bg, tile_subset=subset)
-    # keep the per-Gaussian stage in the autograd graph even when no tile of the sample touches it
-    anchor = pre["xy"].sum() + pre["conic"].sum() + pre["opacity"].sum() + pre["rgb"].sum()
-    return color + 0.0 * anchor
+    return pre, pl, ranges
 
 
-def _matvec_once(model, cam, bg, subset, tangents):
-    # J v (forward mode)
+def _matvec_phases(model, cam, bg, tiles, tangents):
+    """One J v + J^T (2 J v) of the view restricted to `tiles`, timed per phase (seconds):
+    per-Gaussian work on all P (preprocess + binning under forward-AD, again under autograd, and the autograd
+    backward from the screen-space tensors to the parameters) and per-tile work on the sampled tiles only
+    (blend under forward-AD, blend + its backward to the screen-space tensors)."""
+    st = tr.settings_from_camera(cam, bg, model.active_sh_degree)
+    H, W = st.image_height, st.image_width
+    names = ("_features_dc", "_features_rest", "_scaling", "_rotation", "_opacity")
+    saved = tuple(getattr(model, n) for n in names)
+    # J v (forward mode, solver_functions.py:83-99)
     with torch.no_grad(), fwAD.dual_level():
-        saved = (model._features_dc, model._features_rest, model._scaling, model._rotation, model._opacity)
-        model._features_dc = fwAD.make_dual(saved[0], tangents[0])
-        model._features_rest = fwAD.make_dual(saved[1], tangents[1])
-        model._scaling = fwAD.make_dual(saved[2], tangents[2])
-        model._rotation = fwAD.make_dual(saved[3], tangents[3])
-        model._opacity = fwAD.make_dual(saved[4], tangents[4])
+        for n, p, t in zip(names, saved, tangents):
+            setattr(model, n, fwAD.make_dual(p, t))
         try:
-            q = fwAD.unpack_dual(_render_subset(model, cam, bg, subset)).tangent
+            t0 = time.perf_counter()
+            pre, pl, ranges = _preprocess_binning(model, st)
+            t1 = time.perf_counter()
+            q = fwAD.unpack_dual(tr.blend_tiles(pre, pl, ranges, H, W, st.bg, tiles)).tangent
+            t2 = time.perf_counter()
         finally:
-            (model._features_dc, model._features_rest, model._scaling, model._rotation, model._opacity) = saved
-    q = torch.zeros(3, cam.image_height, cam.image_width) if q is None else q
-    # J^T (2 q) (reverse mode)
+            for n, p in zip(names, saved):
+                setattr(model, n, p)
+    q = torch.zeros(0, 3) if q is None else q
+    # J^T (2 q) (reverse mode, solver_functions.py:101-132), the graph cut at the screen-space tensors
     model.zero_grad()
-    color = _render_subset(model, cam, bg, subset)
-    (color * (2.0 * q)).sum().backward()
-    return q
+    t3 = time.perf_counter()
+    pre, pl, ranges = _preprocess_binning(model, st)
+    t4 = time.perf_counter()
+    leaves = {k: pre[k].detach().requires_grad_(pre[k].requires_grad) for k in _SCREEN}
+    color = tr.blend_tiles(dict(pre, **leaves), pl, ranges, H, W, st.bg, tiles)
+    if color.requires_grad:
+        (color * (2.0 * q)).sum().backward()
+    t5 = time.perf_counter()
+    outs = [(pre[k], leaves[k].grad) for k in _SCREEN if leaves[k].grad is not None]
+    if outs:
+        torch.autograd.backward([o for o, _ in outs], [g for _, g in outs])
+    t6 = time.perf_counter()
+    return (t1 - t0) + (t4 - t3) + (t6 - t5), (t2 - t1) + (t5 - t4)
 
 
-def cpu_matvec_rate(model, cam, bg, n_tiles=32, repeats=1, threads=None):
-    """Returns dict(matvec_s, forward_s, t_pre, t_sub, n_tiles, ntiles, threads)."""
+def _forward_phases(model, cam, bg, tiles):
+    st = tr.settings_from_camera(cam, bg, model.active_sh_degree)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        pre, pl, ranges = _preprocess_binning(model, st)
+        t1 = time.perf_counter()
+        tr.blend_tiles(pre, pl, ranges, st.image_height, st.image_width, st.bg, tiles)
+        t2 = time.perf_counter()
+    return t1 - t0, t2 - t1
+
+
+def cpu_matvec_rate(model, cam, bg, n_tiles=64, repeats=3, threads=None):
+    """Seconds per full-frame matvec / forward on the host cores from a bounded sample: the per-Gaussian phases
+    run on all P Gaussians and are timed as they are; the per-tile phases run on `n_tiles` tiles spread uniformly
+    over the frame, timed on their own (no difference of two noisy totals) and scaled by ntiles / n_tiles.
+    Each phase is the median of `repeats` runs.  Returns dict(matvec_s, forward_s, t_gauss, t_tiles, f_gauss,
+    f_tiles, n_tiles, ntiles, threads, cpu_model)."""
     if threads:
         torch.set_num_threads(threads)
     th = torch.get_num_threads()
     W, H = cam.image_width, cam.image_height
     ntiles = ((W + 15) // 16) * ((H + 15) // 16)
     stride = max(1, ntiles // n_tiles)
-    subset = set(range(stride // 2, ntiles, stride))
+    tiles = list(range(stride // 2, ntiles, stride))[:n_tiles]
     g = torch.Generator().manual_seed(3)
     tangents = [torch.randn(t.shape, generator=g) for t in
                 (model._features_dc, model._features_rest, model._scaling, model._rotation, model._opacity)]
 
-    def timed(fn):  # median of `repeats` runs
-        ts = []
-        for _ in range(repeats):
-            t0 = time.perf_counter()
-            fn()
-            ts.append(time.perf_counter() - t0)
-        return sorted(ts)[len(ts) // 2]
+    def med(xs):
+        return sorted(xs)[len(xs) // 2]
 
-    t_pre = timed(lambda: _matvec_once(model, cam, bg, set(), tangents))
-    t_sub = timed(lambda: _matvec_once(model, cam, bg, subset, tangents))
-    with torch.no_grad():
-        f_pre = timed(lambda: _render_subset(model, cam, bg, set()))
-        f_sub = timed(lambda: _render_subset(model, cam, bg, subset))
-    scale = ntiles / len(subset)
-    return dict(matvec_s=t_pre + max(t_sub - t_pre, 0.0) * scale, forward_s=f_pre + max(f_sub - f_pre, 0.0) * scale,
-                t_pre=t_pre, t_sub=t_sub, n_tiles=len(subset), ntiles=ntiles, threads=th,
-                cpu_model=_cpu_model())
+    mv = [_matvec_phases(model, cam, bg, tiles, tangents) for _ in range(repeats)]
+    fw = [_forward_phases(model, cam, bg, tiles) for _ in range(repeats)]
+    t_gauss, t_tiles = med([a for a, _ in mv]), med([b for _, b in mv])
+    f_gauss, f_tiles = med([a for a, _ in fw]), med([b for _, b in fw])
+    scale = ntiles / len(tiles)
+    return dict(matvec_s=t_gauss + t_tiles * scale, forward_s=f_gauss + f_tiles * scale,
+                t_gauss=t_gauss, t_tiles=t_tiles, f_gauss=f_gauss, f_tiles=f_tiles, n_tiles=len(tiles),
+                ntiles=ntiles, threads=th, cpu_model=_cpu_model())
 
 
 def _cpu_model():

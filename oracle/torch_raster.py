@@ -242,6 +242,48 @@ def binning(pre):
     return torch.from_numpy(point_list), torch.from_numpy(tile_sorted), torch.from_numpy(ranges)
 
 
+def _tile_pixels(t, gx, H, W):
+    ty, tx = divmod(t, gx)
+    ys = torch.arange(ty * BLOCK_Y, min((ty + 1) * BLOCK_Y, H))
+    xs = torch.arange(tx * BLOCK_X, min((tx + 1) * BLOCK_X, W))
+    py, px = torch.meshgrid(ys, xs, indexing="ij")
+    return py.reshape(-1), px.reshape(-1)
+
+
+def _blend_tile(xy, conic, opac, rgb, invd, L, px, py, bg):
+    """Front-to-back blend of one tile's pixels over its sorted list L (upstream renderCUDA semantics).
+    Returns (color[npx,3], invdepth[npx], final_T[npx], n_contrib[npx] int32)."""
+    dtype = xy.dtype
+    npx = py.numel()
+    pxf = px.to(dtype)[:, None]
+    pyf = py.to(dtype)[:, None]
+    dx = xy[L, 0][None, :] - pxf
+    dy = xy[L, 1][None, :] - pyf
+    a, b, c = conic[L, 0][None, :], conic[L, 1][None, :], conic[L, 2][None, :]
+    power = -0.5 * (a * dx * dx + c * dy * dy) - b * dx * dy
+    G = torch.exp(power)
+    araw = opac[L][None, :] * G
+    alpha = araw + (torch.clamp_max(araw, 0.99) - araw).detach()
+    with torch.no_grad():
+        ac = torch.clamp_max(araw.detach(), 0.99)
+        valid = (power.detach() <= 0) & (ac >= 1.0 / 255.0)
+        om = torch.where(valid, 1 - ac, torch.ones_like(ac))
+        Tincl = torch.cumprod(om, dim=1)
+        stop = valid & (Tincl < 0.0001)
+        n = L.numel()
+        idx = torch.arange(n)[None, :].expand_as(stop)
+        first_stop = torch.where(stop, idx, torch.full_like(idx, n)).min(dim=1).values
+        contrib = valid & (idx < first_stop[:, None])
+        last = torch.where(contrib, idx + 1, torch.zeros_like(idx)).max(dim=1).values
+    m = contrib.to(dtype)
+    one_m = 1 - m * alpha
+    Tin = torch.cumprod(one_m, dim=1)
+    Tex = torch.cat([torch.ones(npx, 1, dtype=dtype), Tin[:, :-1]], dim=1)
+    wgt = m * alpha * Tex
+    Tfin = Tin[:, -1]
+    return wgt @ rgb[L] + Tfin[:, None] * bg[None, :], wgt @ invd[L], Tfin, last.to(torch.int32)
+
+
 def blend(pre, point_list, ranges, H, W, bg, tile_subset=None):
     """Per-tile front-to-back alpha blending (App. A step 11), dense per tile.
     Returns color[3,H,W], invdepth[1,H,W], final_T[H,W], n_contrib[H,W] (int32)."""
@@ -251,53 +293,22 @@ def blend(pre, point_list, ranges, H, W, bg, tile_subset=None):
     dtype = xy.dtype
     bg = bg.to(dtype).reshape(3)
     pix_chunks, col_chunks, dep_chunks, T_chunks, nc_chunks = [], [], [], [], []
-    for ty in range(gy):
-        for tx in range(gx):
-            t = ty * gx + tx
-            ys = torch.arange(ty * BLOCK_Y, min((ty + 1) * BLOCK_Y, H))
-            xs = torch.arange(tx * BLOCK_X, min((tx + 1) * BLOCK_X, W))
-            py, px = torch.meshgrid(ys, xs, indexing="ij")
-            py, px = py.reshape(-1), px.reshape(-1)
-            pix_chunks.append(py * W + px)
-            s, e = int(ranges[t, 0]), int(ranges[t, 1])
-            npx = py.numel()
-            if e <= s or (tile_subset is not None and t not in tile_subset):
-                col_chunks.append(bg[None, :].expand(npx, 3) * torch.ones(npx, 1, dtype=dtype))
-                dep_chunks.append(torch.zeros(npx, dtype=dtype))
-                T_chunks.append(torch.ones(npx, dtype=dtype))
-                nc_chunks.append(torch.zeros(npx, dtype=torch.int32))
-                continue
-            L = point_list[s:e]
-            pxf = px.to(dtype)[:, None]
-            pyf = py.to(dtype)[:, None]
-            dx = xy[L, 0][None, :] - pxf
-            dy = xy[L, 1][None, :] - pyf
-            a, b, c = conic[L, 0][None, :], conic[L, 1][None, :], conic[L, 2][None, :]
-            power = -0.5 * (a * dx * dx + c * dy * dy) - b * dx * dy
-            G = torch.exp(power)
-            araw = opac[L][None, :] * G
-            alpha = araw + (torch.clamp_max(araw, 0.99) - araw).detach()
-            with torch.no_grad():
-                ac = torch.clamp_max(araw.detach(), 0.99)
-                valid = (power.detach() <= 0) & (ac >= 1.0 / 255.0)
-                om = torch.where(valid, 1 - ac, torch.ones_like(ac))
-                Tincl = torch.cumprod(om, dim=1)
-                stop = valid & (Tincl < 0.0001)
-                n = L.numel()
-                idx = torch.arange(n)[None, :].expand_as(stop)
-                first_stop = torch.where(stop, idx, torch.full_like(idx, n)).min(dim=1).values
-                contrib = valid & (idx < first_stop[:, None])
-                last = torch.where(contrib, idx + 1, torch.zeros_like(idx)).max(dim=1).values
-            m = contrib.to(dtype)
-            one_m = 1 - m * alpha
-            Tin = torch.cumprod(one_m, dim=1)
-            Tex = torch.cat([torch.ones(npx, 1, dtype=dtype), Tin[:, :-1]], dim=1)
-            wgt = m * alpha * Tex
-            Tfin = Tin[:, -1]
-            col_chunks.append(wgt @ rgb[L] + Tfin[:, None] * bg[None, :])
-            dep_chunks.append(wgt @ invd[L])
-            T_chunks.append(Tfin)
-            nc_chunks.append(last.to(torch.int32))
+    for t in range(gx * gy):
+        py, px = _tile_pixels(t, gx, H, W)
+        pix_chunks.append(py * W + px)
+        s, e = int(ranges[t, 0]), int(ranges[t, 1])
+        npx = py.numel()
+        if e <= s or (tile_subset is not None and t not in tile_subset):
+            col_chunks.append(bg[None, :].expand(npx, 3) * torch.ones(npx, 1, dtype=dtype))
+            dep_chunks.append(torch.zeros(npx, dtype=dtype))
+            T_chunks.append(torch.ones(npx, dtype=dtype))
+            nc_chunks.append(torch.zeros(npx, dtype=torch.int32))
+            continue
+        col, dep, Tfin, last = _blend_tile(xy, conic, opac, rgb, invd, point_list[s:e], px, py, bg)
+        col_chunks.append(col)
+        dep_chunks.append(dep)
+        T_chunks.append(Tfin)
+        nc_chunks.append(last)
     pix = torch.cat(pix_chunks)
     inv = torch.empty_like(pix)
     inv[pix] = torch.arange(pix.numel())
@@ -306,6 +317,23 @@ def blend(pre, point_list, ranges, H, W, bg, tile_subset=None):
     final_T = torch.cat(T_chunks).index_select(0, inv).reshape(H, W)
     n_contrib = torch.cat(nc_chunks).index_select(0, inv).reshape(H, W)
     return color, invdepth, final_T, n_contrib
+
+
+def blend_tiles(pre, point_list, ranges, H, W, bg, tiles):
+    """The colours of the listed tiles only (nothing is done for the others): [sum of their pixels, 3], the
+    per-tile arithmetic of blend() -- the bounded sample of the CPU baseline (oracle/cpu_baseline.py)."""
+    gx, _ = pre["grid"]
+    xy, conic, opac, rgb = pre["xy"], pre["conic"], pre["opacity"], pre["rgb"]
+    invd = 1.0 / pre["depth"]
+    bg = bg.to(xy.dtype).reshape(3)
+    out = []
+    for t in tiles:
+        s, e = int(ranges[t, 0]), int(ranges[t, 1])
+        if e <= s:
+            continue
+        py, px = _tile_pixels(t, gx, H, W)
+        out.append(_blend_tile(xy, conic, opac, rgb, invd, point_list[s:e], px, py, bg)[0])
+    return torch.cat(out, dim=0) if out else torch.zeros(0, 3, dtype=xy.dtype) + 0.0 * xy.sum()
 
 
 def rasterize(means3D, means2D, opacities, st, shs=None, colors_precomp=None, scales=None,
