@@ -249,7 +249,8 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
-        const bool valid = inside && contributor < st.last && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
+        const bool c_last = contributor < st.last, c_pow = !(power > 0.0f), c_alpha = alpha >= 1.0f / 255.0f;
+        const bool valid = c_last && c_pow && c_alpha;  // st.last = 0 outside the image
         // <colour, dL/dpix> for every lane (the colour is already in registers)
         float cd;
         {
@@ -261,7 +262,9 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         // values are 0, T is unchanged (rcp(1) = 1), and the pending <acc, u> update it applies early is the
         // one the next blended entry would apply with the same operands (it then adds 0 * (...)).  No
         // per-lane branch and no zeroing of the row values per visit.
-        const bool any = __ballot(valid) != 0ull;
+        // (per-condition ballots fold into their compares' lane masks: no VGPR round trip of `valid`)
+        const bool any = (__builtin_amdgcn_ballot_w64(c_last) & __builtin_amdgcn_ballot_w64(c_pow) &
+                          __builtin_amdgcn_ballot_w64(c_alpha)) != 0ull;
         float gv[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) gv[q] = 0.f;
@@ -311,10 +314,12 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           if (any) {
             float pv[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) pv[k] = 0.f;
-#pragma unroll
             for (int q = 0; q < NV; ++q)
               if (q_used<WITH_XY, WITH_INV>(q)) pv[q_slot<WITH_XY, WITH_INV>(q)] = gv[q];
+            // unused slots (7 with the LM rows) are never stored: any register will do, and slot k - 4 pairs
+            // with it in the first permlane step anyway (no zero materialised per visit)
+#pragma unroll
+            for (int k = NU; k < 8; ++k) pv[k] = pv[k - 4];
             rr = wave_reduce8_t(pv, lane);
           }
           const int k = lane >> 3;

@@ -91,9 +91,10 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
           const float dalpha = G * (D.x + b.y * dpower);
           const float wt = alpha * o.T;
           const float dw = dalpha * o.T + alpha * o.dT;
-          o.dC[0] += D.y * wt + b.z * dw;
-          o.dC[1] += D.z * wt + b.w * dw;
-          o.dC[2] += D.w * wt + C.x * dw;
+          // two FMAs into the accumulator per channel (not mul + fma + add)
+          o.dC[0] = fmaf(b.z, dw, fmaf(D.y, wt, o.dC[0]));
+          o.dC[1] = fmaf(b.w, dw, fmaf(D.z, wt, o.dC[1]));
+          o.dC[2] = fmaf(C.x, dw, fmaf(D.w, wt, o.dC[2]));
           o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
           o.T = o.T * (1.f - alpha);
         }
@@ -190,9 +191,10 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
         const float dalpha = G * (D.x + b.y * dpower);
         const float wt = alpha * o.T;
         const float dw = dalpha * o.T + alpha * o.dT;
-        o.dC[0] += D.y * wt + b.z * dw;
-        o.dC[1] += D.z * wt + b.w * dw;
-        o.dC[2] += D.w * wt + C.x * dw;
+        // two FMAs into the accumulator per channel (not mul + fma + add)
+        o.dC[0] = fmaf(b.z, dw, fmaf(D.y, wt, o.dC[0]));
+        o.dC[1] = fmaf(b.w, dw, fmaf(D.z, wt, o.dC[1]));
+        o.dC[2] = fmaf(C.x, dw, fmaf(D.w, wt, o.dC[2]));
         o.dT = o.dT * (1.f - alpha) - o.T * dalpha;
         o.T = o.T * (1.f - alpha);
       }
