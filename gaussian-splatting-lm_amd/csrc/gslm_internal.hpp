@@ -33,14 +33,25 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // ---------------- radix sort (LSD, 8-bit digits, stable) ----------------
 constexpr int SORT_THREADS = 256;
-#ifndef GSLM_SORT_ITEMS
-#define GSLM_SORT_ITEMS 16
-#endif
-constexpr int SORT_ITEMS = GSLM_SORT_ITEMS;          // items per thread per block
+constexpr int SORT_ITEMS = 16;                       // items per thread per block (large sorts)
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS; // 4096 keys per block
+// Sorts that would launch fewer than SORT_FULL_BLOCKS blocks of SORT_TILE keys (the depth sort of 1M
+// Gaussians: 245 blocks, one per CU, one wave per SIMD) use SORT_ITEMS_SMALL items per thread instead, so
+// the launch fills the chip's 256 CUs several times over.
+#ifndef GSLM_SORT_ITEMS_SMALL
+#define GSLM_SORT_ITEMS_SMALL 8
+#endif
+constexpr int SORT_ITEMS_SMALL = GSLM_SORT_ITEMS_SMALL;
+constexpr int64_t SORT_FULL_BLOCKS = 1024;
 constexpr int RADIX = 256;
 
-inline int64_t sort_blocks(int64_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+inline int sort_items(int64_t n) {
+  return (n + SORT_TILE - 1) / SORT_TILE >= SORT_FULL_BLOCKS ? SORT_ITEMS : SORT_ITEMS_SMALL;
+}
+inline int64_t sort_blocks(int64_t n) {
+  const int64_t t = (int64_t)SORT_THREADS * sort_items(n);
+  return (n + t - 1) / t;
+}
 inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_blocks(n) * 4 + 4 * RADIX; }
 
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the

@@ -40,6 +40,7 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
   return inc + off;
 }
 
+template <int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n,
                                                              int shift, uint32_t dmask, uint32_t* __restrict__ hist,
                                                              int nblocks) {
@@ -47,9 +48,9 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __r
   const int tid = threadIdx.x;
   cnt[tid] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+  const int64_t base = (int64_t)blockIdx.x * (SORT_THREADS * ITEMS);
 #pragma unroll 4
-  for (int r = 0; r < SORT_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const int64_t i = base + r * SORT_THREADS + tid;
     if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
   }
@@ -82,29 +83,31 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // counts into local positions: block order = wave order, round order, lane order = input order (stable).  The
 // keys are reordered through LDS into digit runs and each run is written to its global offset by consecutive
 // threads (coalesced segments instead of one scattered 4-byte store per key).
+template <int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
     const uint32_t* __restrict__ totals) {
   static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
-  constexpr int WAVE_KEYS = SORT_TILE / 4;
-  __shared__ uint32_t s_keys[SORT_TILE], s_vals[SORT_TILE];
+  constexpr int TILE = SORT_THREADS * ITEMS;
+  constexpr int WAVE_KEYS = TILE / 4;
+  __shared__ uint32_t s_keys[TILE], s_vals[TILE];
   __shared__ uint32_t s_wcnt[4][RADIX];  // per-wave running digit count, then the wave's offset in the digit run
   __shared__ uint32_t s_loc[RADIX];      // block-local start of each digit's run
   __shared__ uint32_t s_gbase[RADIX];    // global offset of this block's run of each digit
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
-  const int nvalid = (int)min<int64_t>(SORT_TILE, n - base);
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int nvalid = (int)min<int64_t>(TILE, n - base);
   const int wbase = w * WAVE_KEYS;
   const uint32_t dmask = (1u << nbits) - 1u;
 
 #pragma unroll
   for (int k = 0; k < 4; ++k) s_wcnt[w][lane + 64 * k] = 0u;
   // all loads first (16 keys + 16 values per lane in flight), wave w on keys [wbase, wbase + 1024) of the block
-  uint32_t key[SORT_ITEMS], val[SORT_ITEMS], lrank[SORT_ITEMS];
+  uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const int64_t i = base + wbase + r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
     val[r] = i < n ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == NULL: the values are the indices
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   // 1. wave-local stable rank of every key among equal digits
   const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const bool valid = wbase + r * 64 + lane < nvalid;
     const uint32_t d = (key[r] >> shift) & dmask;
     unsigned long long m = __ballot(valid);
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     if (wbase + r * 64 + lane < nvalid) {
       const uint32_t d = (key[r] >> shift) & dmask;
       const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
@@ -329,6 +332,7 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const int nb = (int)sort_blocks(n);
+  const bool small = sort_items(n) != SORT_ITEMS;
   uint32_t* totals = hist + (size_t)RADIX * nb;
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
@@ -340,11 +344,18 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
   for (int shift = 0; shift < end_bit; shift += per) {
     const int nbits = end_bit - shift < per ? end_bit - shift : per;  // digit bits of this pass
     const uint32_t dmask = (1u << nbits) - 1u;
-    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
-    hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, ki,
-                       (first && iota_values) ? (const uint32_t*)nullptr : vi, ko, vo, n, shift, nbits, hist, nb,
-                       totals);
+    const uint32_t* vin = (first && iota_values) ? (const uint32_t*)nullptr : vi;
+    if (small) {
+      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
+      hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+      hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift,
+                         nbits, hist, nb, totals);
+    } else {
+      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
+      hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+      hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift, nbits,
+                         hist, nb, totals);
+    }
     first = false;
     GSLM_LAUNCH_CHECK();
     std::swap(ki, ko);
