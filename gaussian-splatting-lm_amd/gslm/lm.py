@@ -260,18 +260,25 @@ class LMProblem:
         self.matvec_dot(v, y, None)
         return y
 
-    def matvec_dot(self, v, y, dot_out, pre=None):
+    # cgls_fused may pass exposure_zero=True (see matvec_dot)
+    supports_exposure_zero = True
+
+    def matvec_dot(self, v, y, dot_out, pre=None, exposure_zero=False):
         """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
         view; exposure components of v zero, as in every LM iterate).  Returns True if fused.
         pre = (s, beta_num_ptr, beta_den_ptr): first v <- s + beta v (the deferred CG direction
-        update), fused into the first view's tangent kernel."""
+        update), fused into the first view's tangent kernel.
+        exposure_zero: the caller guarantees that the exposure components of v (after pre) and of y are
+        zero already -- true of every CG iterate (J has no exposure column, x0 = 0, y is the solver's own
+        q) -- so y's exposure slice D v = 0 is left as it is (no elementwise launch per product)."""
         fuse = dot_out is not None and len(self.views) == 1
-        self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None, pre=pre)
+        self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None, pre=pre,
+                                 exposure_zero=exposure_zero)
         return fuse
 
-    def local_normal_matvec(self, v, y, damp=False, dot_out=None, pre=None):
+    def local_normal_matvec(self, v, y, damp=False, dot_out=None, pre=None, exposure_zero=False):
         """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y).
-        pre: see matvec_dot."""
+        pre, exposure_zero: see matvec_dot."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
         ys = self.layout.grads_struct(y)
@@ -305,7 +312,9 @@ class LMProblem:
                                           vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts), self.stream),
                   "gslm_matvec_view_ex")
             vr.tail_clean = True
-        if damp:
+        if exposure_zero:
+            pass  # y[e0:e1] = D v[e0:e1] = 0 already (matvec_dot)
+        elif damp:
             torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
         else:
             y[e0:e1].zero_()
@@ -551,7 +560,10 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             full = None if pre is None else pre + ((x, pend[0], pend[1]) if pend is not None else (None, None, None))
             if full is not None:
                 pend = None
-            if not prob.matvec_dot(p, q, ptr(DEL), pre=full):
+            # (q was allocated zero and, like every iterate, has zero exposure components: J has no exposure
+            # column and x0 = 0)
+            ez = {"exposure_zero": True} if getattr(prob, "supports_exposure_zero", False) else {}
+            if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
             reduce(DEL)
             if check_every and sc[DEL].item() < 1e-20:

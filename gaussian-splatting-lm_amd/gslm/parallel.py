@@ -66,6 +66,7 @@ def _staged(fn, *tensors):
 
 class ShardedOperator:
     SCREEN_FLOATS = 8  # per (view, Gaussian) in the screen exchange
+    supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
 
     def __init__(self, local, group=None, all_cams=None, exchange="auto"):
         self.local = local
@@ -161,6 +162,7 @@ def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto"
     if exchange == "auto" and n > 1 and all_cams is not None and len(cams) >= 1 and \
             len(all_cams) == n * len(cams) and local.mask_xyz and not local.ssim:
         exchange = "gaussian"
+    supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
     if exchange == "gaussian":
         if local.ssim or not local.mask_xyz:
             raise ValueError("the Gaussian-sharded exchange runs the disable_ssim product with xyz frozen")
@@ -208,6 +210,7 @@ class GaussianShardedOperator:
     the shard, which exercises the same shard layout, scalar reductions and gathers."""
 
     exchange = "gaussian"
+    supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
 
     def __init__(self, local, group=None, all_cams=None):
         self.local = local
