@@ -162,7 +162,6 @@ def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto"
     if exchange == "auto" and n > 1 and all_cams is not None and len(cams) >= 1 and \
             len(all_cams) == n * len(cams) and local.mask_xyz and not local.ssim:
         exchange = "gaussian"
-    supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
     if exchange == "gaussian":
         if local.ssim or not local.mask_xyz:
             raise ValueError("the Gaussian-sharded exchange runs the disable_ssim product with xyz frozen")
