@@ -86,7 +86,15 @@ def main():
     # collectives); the driver's runs use RCCL ("nccl"), one rank per GPU.
     backend = os.environ.get("GSLM_BENCH_DIST", "nccl")
     dev_index = local_rank if backend == "nccl" else local_rank % max(torch.cuda.device_count(), 1)
-    if world_size > 1:
+    # GSLM_FORCE_COLLECTIVES=1 at one rank (the one-rank RCCL rehearsal, gslm.parallel.collectives_on): a one-rank
+    # process group, every collective of the exchange picked by GSLM_BENCH_EXCHANGE (default "auto") issued to it
+    forced = os.environ.get("GSLM_FORCE_COLLECTIVES") == "1"
+    if world_size > 1 or forced:
+        if forced and world_size == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(dev_index)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
@@ -124,7 +132,8 @@ def main():
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
     # one view per problem (N = 1): the SH-rest group of the CG vectors is carried as its 3 coordinates in
     # the view's SH-rest span (GSLM_MV_SH_REST_PROJECTED); several views: the full layout
-    prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device, sh_projection="auto")
+    prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device, sh_projection="auto",
+                            exchange=os.environ.get("GSLM_BENCH_EXCHANGE", "auto"))
     prob.evaluate()
     g = prob.rhs(prob.zeros())
     torch.cuda.synchronize()
@@ -291,7 +300,7 @@ def main():
     # (at configs[4], 5M Gaussians x 32 4K views, that is ~100 GB)
     n_views_local = len(loc.views)
     sh_proj = prob.layout.rest_projected
-    exchange = prob.exchange if world_size > 1 else "none"
+    exchange = prob.exchange if (world_size > 1 or forced) else "none"
     del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
 
@@ -376,7 +385,7 @@ def main():
             "cg_full_layout": cg_full,
         }
         print(json.dumps(line), flush=True)
-    if world_size > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -21,6 +21,7 @@ the GPU, oracle.lm_ref.OracleLMProblem in the CPU tests; the screen exchange nee
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -32,6 +33,13 @@ def world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def collectives_on(world_size):
+    """Whether the cross-rank collectives run: several ranks, or GSLM_FORCE_COLLECTIVES=1 with one rank -- the
+    one-rank RCCL rehearsal on a one-GPU box (tests/test_gpu_rccl.py): every device-tensor collective of the
+    multi-GPU path then goes through the backend (a copy with one rank) instead of the single-rank shortcut."""
+    return world_size > 1 or os.environ.get("GSLM_FORCE_COLLECTIVES") == "1"
 
 
 def shard_views(n_views, rank, world_size):
@@ -77,7 +85,7 @@ class ShardedOperator:
         self._screen = None
 
     def _pick_exchange(self, mode):
-        if self.world_size == 1 or mode == "allreduce":
+        if not collectives_on(self.world_size) or mode == "allreduce":
             return "allreduce"
         capable = self.all_cams is not None and getattr(self.local, "mask_xyz", False) and \
             hasattr(self.local, "screen_products") and not getattr(self.local, "ssim", False)
@@ -97,7 +105,7 @@ class ShardedOperator:
         return getattr(self.local, name)
 
     def _allreduce(self, t):
-        if self.world_size > 1:
+        if collectives_on(self.world_size):
             _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
         return t
 
@@ -117,7 +125,7 @@ class ShardedOperator:
 
     def matvec_dot(self, v, y, dot_out, pre=None):
         kw = {} if pre is None else {"pre": pre}
-        if self.world_size == 1:
+        if not collectives_on(self.world_size):
             return self.local.matvec_dot(v, y, dot_out, **kw)
         if self.exchange == "screen":
             return self._matvec_screen(v, y, dot_out, pre)
@@ -156,8 +164,10 @@ def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto"
     ShardedOperator's own choice."""
     from gslm.lm import LMProblem
     rank, n = world()
-    if n > 1 or (all_cams is not None and len(all_cams) > 1):
-        kw["sh_projection"] = False  # the SH-rest span is one view's: the global batch has several
+    if n > 1 or (all_cams is not None and len(all_cams) > 1) or exchange == "gaussian":
+        # the SH-rest span is one view's: the global batch has several (and the Gaussian-sharded exchange
+        # runs on the full layout)
+        kw["sh_projection"] = False
     local = LMProblem(model, cams, bg, **kw)
     if exchange == "auto" and n > 1 and all_cams is not None and len(cams) >= 1 and \
             len(all_cams) == n * len(cams) and local.mask_xyz and not local.ssim:
@@ -248,12 +258,12 @@ class GaussianShardedOperator:
 
     # ------------------------------------------------------------------ collectives
     def _allreduce(self, t):
-        if self.world_size > 1:
+        if collectives_on(self.world_size):
             _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
         return t
 
     def _all_to_all(self, out, inp):
-        if self.world_size == 1:
+        if not collectives_on(self.world_size):
             out.copy_(inp)
             return
         _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
@@ -262,7 +272,7 @@ class GaussianShardedOperator:
         """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks.  One slot (the CG
         loop's delta and gamma' without the residual monitor): in place on the 8-byte view, no gather / scatter
         kernels and no host-to-device index copy around the collective."""
-        if self.world_size == 1:
+        if not collectives_on(self.world_size):
             return
         slots = tuple(slots)
         if len(slots) == 1:
@@ -306,7 +316,7 @@ class GaussianShardedOperator:
             pack[:self.hi - self.lo, c:c + w] = rows[name]
             c += w
         allp = torch.empty(n * S, F, dtype=vec.dtype, device=vec.device)
-        if n > 1:
+        if collectives_on(n):
             _all_gather_into(allp, pack, self.group)
         else:
             allp.copy_(pack)
@@ -320,7 +330,7 @@ class GaussianShardedOperator:
         if self.layout.n_exposure:
             a0, a1 = self.layout.offsets["exposure"]
             out[e0:e1] = vec[a0:a1]
-        if n > 1:
+        if collectives_on(n):
             ex = out[e0:e1].clone()
             self._allreduce(ex)
             out[e0:e1] = ex

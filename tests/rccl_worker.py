@@ -1,0 +1,47 @@
+"""Worker of tests/test_gpu_rccl.py (run as its own process, not collected by pytest): one rank of a "nccl"
+(RCCL) process group with GSLM_FORCE_COLLECTIVES=1, so the multi-GPU path's device-tensor collectives
+(all_to_all_single, all_gather_into_tensor, all_reduce of CG scalars and vectors) run through RCCL on the one
+GPU of the box.  Each exchange's loss, J^T b, product and 3 CG iterates are compared with the single-process
+LMProblem; prints one JSON line with the backend, the exchanges run and their errors."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    os.environ["GSLM_FORCE_COLLECTIVES"] = "1"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from gslm.lm import LMProblem
+    from gslm.parallel import ShardedLMProblem
+    from test_gpu_dist import _run, _scene
+    out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "exchanges": {}}
+    for mode, nv in (("gaussian", 2), ("screen", 2), ("allreduce", 2)):
+        model, cams = _scene(nv, 4001)
+        model = model.to("cuda")
+        for c in cams:
+            c.to("cuda")
+        ref_op = LMProblem(model, cams, torch.zeros(3))
+        ref = _run(ref_op, ref_op.layout)
+        op = ShardedLMProblem(model, cams, torch.zeros(3), all_cams=cams, exchange=mode)
+        assert op.exchange == mode, (op.exchange, mode)
+        got = _run(op, op.layout)
+        out["exchanges"][mode] = {
+            "loss_rel": abs(float(got["loss"]) - float(ref["loss"])) / float(ref["loss"]),
+            "g_max": float((got["g"] - ref["g"]).abs().max() / ref["g"].abs().max()),
+            "y_max": float((got["y"] - ref["y"]).abs().max() / ref["y"].abs().max()),
+            "x_rel": float((got["x"] - ref["x"]).norm() / ref["x"].norm()),
+        }
+    dist.barrier()
+    dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
