@@ -76,6 +76,11 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
+    # stdout carries exactly the one JSON line: everything else written to fd 1 -- RCCL prints its version banner
+    # there at communicator setup -- goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     if world_size != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_size}: launch one rank per GPU "
@@ -384,7 +389,8 @@ def main():
             "first_order": fo,
             "cg_full_layout": cg_full,
         }
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
