@@ -246,7 +246,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       {
         const uint32_t contributor = (uint32_t)(base - j);  // 0-based list position
         const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float power = gpower(a.z, a.w, b.x, dx, dy);
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
         const bool c_last = contributor < st.last, c_pow = !(power > 0.0f), c_alpha = alpha >= 1.0f / 255.0f;

@@ -82,7 +82,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
                      "v"(D.w));
         const uint32_t pos = (uint32_t)(r * BATCH + j);
         const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+        const float power = gpower(a.z, a.w, b.x, dx, dy);
         const float G = gexp(power);
         const float alpha = fminf(0.99f, b.y * G);
         if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
@@ -110,7 +110,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
                    "v"(b.w), "v"(cc.x));
       const uint32_t pos = (uint32_t)(r * BATCH + j);
       const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
 #ifdef GSLM_EXPERIMENT_COUNT
@@ -182,7 +182,7 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
                    "v"(D.w));
       const uint32_t pos = (uint32_t)(base + j);
       const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
       if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       const float4 a = s[j], b = s[64 + j], cc = s[128 + j];
       asm volatile("" : : "v"(b.z), "v"(b.w), "v"(cc.x), "v"(cc.y));
       const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float alpha = fminf(0.99f, b.y * gexp(power));
       const float test_T = T * (1.0f - alpha);
       if (!done && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
