@@ -147,9 +147,11 @@ struct VjpPix {
   float bg_dot;     // <bg, dL/dpix>
   // Upstream keeps the colour (and inverse depth) accumulated behind the current Gaussian per channel,
   // but only its dot product with dL/dpix enters dL/dalpha; the recurrence is linear, so the dot
-  // itself is carried: accd = <acc, dL/dpix> (+ acc_inv dL/dinvdepth), last_cd = the previous
-  // Gaussian's <colour, dL/dpix> (+ invdepth term).
-  float accd, last_alpha, last_cd;
+  // itself is carried: accd = <acc, dL/dpix> (+ acc_inv dL/dinvdepth).  Upstream folds the previous
+  // Gaussian in at the start of the next visit (accum = last_alpha last_colour + (1 - last_alpha) accum);
+  // here each visit folds its own Gaussian in at its end -- the same operands and FMA, so the same values,
+  // without carrying last_alpha / last_colour across iterations.
+  float accd;
   float tb;         // -T_final <bg, dL/dpix>: the background term of dL/dalpha is tb / (1 - alpha)
 };
 
@@ -163,8 +165,6 @@ __device__ __forceinline__ void vjp_init(VjpPix& s, const ViewK& v, bool inside,
   s.bg_dot = (v.bg[0] * d0 + v.bg[1] * d1) + v.bg[2] * d2;
   s.tb = -s.T_final * s.bg_dot;
   s.accd = 0.f;
-  s.last_alpha = 0.f;
-  s.last_cd = 0.f;
 }
 
 // LDS floats needed by vjp_tile's per-wave partial sums: [wave][value slot][batch element], rows padded
@@ -259,9 +259,8 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           if (WITH_INV) cd += c.y * st.dinv;
         }
         // A visit some lane blends runs the body in every lane, an invalid lane with alpha = G = 0: its row
-        // values are 0, T is unchanged (rcp(1) = 1), and the pending <acc, u> update it applies early is the
-        // one the next blended entry would apply with the same operands (it then adds 0 * (...)).  No
-        // per-lane branch and no zeroing of the row values per visit.
+        // values are 0, T is unchanged (rcp(1) = 1) and its accumulation update adds 0 * (...).  No per-lane
+        // branch and no zeroing of the row values per visit.
         // (per-condition ballots fold into their compares' lane masks: no VGPR round trip of `valid`)
         const bool any = (__builtin_amdgcn_ballot_w64(c_last) & __builtin_amdgcn_ballot_w64(c_pow) &
                           __builtin_amdgcn_ballot_w64(c_alpha)) != 0ull;
@@ -277,14 +276,13 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           const float inv1ma = rcp_f(1.f - a_e);
           st.T = st.T * inv1ma;
           const float dchannel = a_e * st.T;
-          st.accd = st.accd + st.last_alpha * (st.last_cd - st.accd);
-          st.last_cd = cd;
 #pragma unroll
           for (int ch = 0; ch < 3; ++ch) gv[6 + ch] = dchannel * st.dpix[ch];
           if (WITH_INV) gv[9] = dchannel * st.dinv;
           // dL/dalpha = (<c, u> - acc) T - T_final / (1 - alpha) <bg, u>   (tb = -T_final <bg, u>)
-          const float dL_dalpha = (cd - st.accd) * st.T + st.tb * inv1ma;
-          st.last_alpha = a_e;
+          const float cd_acc = cd - st.accd;
+          const float dL_dalpha = cd_acc * st.T + st.tb * inv1ma;
+          st.accd = st.accd + a_e * cd_acc;  // this Gaussian joins the accumulation behind the next one
           gv[5] = G_e * dL_dalpha;
           // h = G dL/dG with G = exp(power): dL/dpower = h; the conic rows carry h dx^2, h dx dy, h dy^2
           // and their constant factors (-1/2, -1, -1/2) are applied once per row at the combine
