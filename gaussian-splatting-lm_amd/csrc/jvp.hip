@@ -87,7 +87,7 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
         const float alpha = fminf(0.99f, b.y * G);
         if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
 #pragma clang fp contract(fast)
-          const float dpower = (C.y * dx * dx + C.w * dy * dy) + C.z * dx * dy;
+          const float dpower = fmaf(dx, fmaf(C.y, dx, C.z * dy), C.w * dy * dy);  // 5 VALU, not 6
           const float dalpha = G * (D.x + b.y * dpower);
           const float wt = alpha * o.T;
           const float dw = dalpha * o.T + alpha * o.dT;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
       const float alpha = fminf(0.99f, b.y * G);
       if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
 #pragma clang fp contract(fast)
-        const float dpower = (C.y * dx * dx + C.w * dy * dy) + C.z * dx * dy;
+        const float dpower = fmaf(dx, fmaf(C.y, dx, C.z * dy), C.w * dy * dy);  // 5 VALU, not 6
         const float dalpha = G * (D.x + b.y * dpower);
         const float wt = alpha * o.T;
         const float dw = dalpha * o.T + alpha * o.dT;
