@@ -68,7 +68,30 @@ def spawn_ranks(args):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
-    codes = [p.wait() for p in procs]
+    # poll every rank: the first one that fails ends the others (survivors would block in a collective until
+    # RCCL's own timeout), and the whole job has a deadline
+    deadline = time.monotonic() + float(os.environ.get("GSLM_BENCH_TIMEOUT_S", "1500"))
+    codes = [None] * len(procs)
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        failed = [c for c in codes if c not in (None, 0)]
+        if failed or time.monotonic() > deadline:
+            if not failed:
+                print("bench.py: ranks still running after the deadline, terminating", file=sys.stderr)
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            return (failed or [124])[0]
+        time.sleep(0.2)
     return max(codes, key=abs)
 
 

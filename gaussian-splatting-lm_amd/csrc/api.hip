@@ -191,21 +191,9 @@ int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
   // a pinned word per host thread: the read-back is one DMA + stream sync instead of a staged pageable copy
   thread_local uint32_t* pinned = nullptr;
   if (!pinned) GSLM_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t), hipHostMallocDefault));
-#ifdef GSLM_EXPERIMENT_NOSYNC
-  // experiment build only: the previous read-back's value, no device round trip (measures its cost on a
-  // scene whose N does not change)
-  // (armed by the GSLM_EXP_NOSYNC_ARM environment variable around a loop over one fixed geometry)
-  static int64_t cached = -1;
-  const bool armed = getenv("GSLM_EXP_NOSYNC_ARM") != nullptr;
-  if (!armed) cached = -1;
-  if (armed && cached >= 0) { *out = cached; return GSLM_OK; }
-#endif
   GSLM_HIP_CHECK(hipMemcpyAsync(pinned, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   GSLM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   *out = (int64_t)*pinned;
-#ifdef GSLM_EXPERIMENT_NOSYNC
-  if (armed) cached = *out;
-#endif
   return GSLM_OK;
 }
 

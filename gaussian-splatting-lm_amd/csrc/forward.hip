@@ -208,7 +208,7 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
   hipLaunchKernelGGL(k_row_flags, dim3(nb), dim3(256), 0, s, N, v.gx, bb.keys_sorted, bb.point_list, bb.ranges,
                      bb.tile_neff, gb.goff, gb.rect, bb.slots, sb.hscan);
   GSLM_LAUNCH_CHECK();
-  // in place: every thread reads its elements before writing them
+  // in place (exclusive_scan_u32 picks k_scan_apply_inplace: no __restrict__ aliasing of in and out)
   const int st = exclusive_scan_u32(sb.hscan, nullptr, sb.hscan, N, sb.scan_tmp, sb.hscan + N, s);
   if (st) return st;
   hipLaunchKernelGGL(k_row_final, dim3(nb), dim3(256), 0, s, N, sb.hscan, bb.slots);

@@ -9,6 +9,13 @@
 #include <stdint.h>
 #include "gslm.h"
 
+// The product library has no experiment branches: a build that skips or stubs out part of a product kernel
+// (the round-1/2 timing experiments) computes wrong results, so such flags are refused outright.
+#if defined(GSLM_EXPERIMENT_COUNT) || defined(GSLM_EXPERIMENT_TIMELINE) || defined(GSLM_EXPERIMENT_SKIP_JVP) || \
+    defined(GSLM_EXPERIMENT_SKIP_VJP) || defined(GSLM_EXPERIMENT_NOSYNC)
+#error "GSLM_EXPERIMENT_* flags are not part of the product build (libgslm.so)"
+#endif
+
 namespace gslm {
 
 constexpr int TILE_X = 16;

@@ -12,11 +12,6 @@
 
 namespace gslm {
 
-#if defined(GSLM_EXPERIMENT_COUNT) || defined(GSLM_EXPERIMENT_TIMELINE)
-static __device__ unsigned long long g_dbg[8];  // experiment builds only: tile-pass iteration counters
-static __device__ unsigned long long g_tile_t[3 * 65536];  // per-tile start / JVP end / VJP end (wall clock)
-#endif
-
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 __device__ __forceinline__ float dpp_f(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, BANK_MASK, true));
@@ -296,16 +291,6 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           gv[3] = hdx * dy;
           gv[4] = hdy * dy;
         }
-#ifdef GSLM_EXPERIMENT_COUNT
-        {
-          const uint64_t vb = __ballot(valid);
-          if (lane == 0) {
-            atomicAdd(&g_dbg[2], 1ull);
-            atomicAdd(&g_dbg[3], (unsigned long long)__popcll(vb));
-            if (!any) atomicAdd(&g_dbg[4], 1ull);
-          }
-        }
-#endif
         if constexpr (NU <= 8) {
           // transposed reduction: value slot k ends in lanes 8k..8k+7; lane 8k stores it
           float rr = 0.f;

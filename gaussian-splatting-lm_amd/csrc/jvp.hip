@@ -113,15 +113,6 @@ __device__ __forceinline__ void jvp_tile(JvpPix& o, bool inside, float pxf, floa
       const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
-#ifdef GSLM_EXPERIMENT_COUNT
-      {
-        const uint64_t vb = __ballot(pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f);
-        if ((threadIdx.x & 63) == 0) {
-          atomicAdd(&g_dbg[0], 1ull);
-          atomicAdd(&g_dbg[1], (unsigned long long)__popcll(vb));
-        }
-      }
-#endif
       if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
         // the tangent arithmetic decides nothing (stop is frozen at the primal): FMA-contracted
 #pragma clang fp contract(fast)
@@ -299,9 +290,6 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   float4* s_t1 = s_t0 + B;
   float2* s_t2 = reinterpret_cast<float2*>(s_t1 + B);
   const int tile = (int)tile_order[blockIdx.x];
-#ifdef GSLM_EXPERIMENT_TIMELINE
-  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile] = wall_clock64();
-#endif
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;
   int px, py;
@@ -320,9 +308,6 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
     w2 = weight[2 * HW + pid];
   }
   JvpPix o;
-#ifdef GSLM_EXPERIMENT_SKIP_JVP
-  o.dC[0] = o.dC[1] = o.dC[2] = o.dT = 1e-3f;
-#else
   if constexpr (WITH_XY) {
     jvp_tile<WITH_XY, false, B>(o, inside, (float)px, (float)py, tile_x, tile_y, last, range, point_list, rec, trec,
                                 s_r0, s_r1, s_r2, s_t0, s_t1, s_t2, s_bits, s_cnt);
@@ -332,27 +317,14 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
     jvp_wave_packed(o, (float)px, (float)py, inside ? last : 0u, wm, q, point_list + range.x, rec, trec,
                     s_lds + 256 * q);
   }
-#endif
   // u = 2 * w (.) (J v)   -- factor 2: the [r; r] residual aliasing of batch_training_loss.py:17
   const float u0 = 2.f * w0 * (o.dC[0] + o.dT * v.bg[0]);
   const float u1 = 2.f * w1 * (o.dC[1] + o.dT * v.bg[1]);
   const float u2 = 2.f * w2 * (o.dC[2] + o.dT * v.bg[2]);
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
-#ifdef GSLM_EXPERIMENT_SKIP_VJP
-  if (u0 + u1 + u2 == 12345.f) contrib[0] = make_float4(u0, u1, u2, 0.f);
-#else
-#ifdef GSLM_EXPERIMENT_TIMELINE
-  __syncthreads();
-  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 1] = wall_clock64();
-#endif
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
                                             slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib, write_tail != 0);
-#ifdef GSLM_EXPERIMENT_TIMELINE
-  __syncthreads();
-  if (threadIdx.x == 0 && tile < 65536) g_tile_t[3 * tile + 2] = wall_clock64();
-#endif
-#endif
 }
 
 // ------------------------------------------------------------------ launchers
@@ -408,17 +380,3 @@ int launch_matvec_render(const ViewK& v, const GaussK& t, const GeomBufs& gb, co
 }
 
 }  // namespace gslm
-#if defined(GSLM_EXPERIMENT_COUNT) || defined(GSLM_EXPERIMENT_TIMELINE)
-extern "C" int gslm_dbg_tiles(unsigned long long* out, int n) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(gslm::g_tile_t), sizeof(unsigned long long) * 3 * n);
-  return 0;
-}
-extern "C" int gslm_dbg_read(unsigned long long* out, int reset) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(gslm::g_dbg), sizeof(unsigned long long) * 8);
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    hipMemcpyToSymbol(HIP_SYMBOL(gslm::g_dbg), z, sizeof(z));
-  }
-  return 0;
-}
-#endif

@@ -13,6 +13,15 @@ namespace gslm {
 
 namespace {
 
+// Orders a wave's LDS stores before its later loads of other lanes' slots: a wave's LDS operations complete in
+// order, so this costs no instruction; it only stops the compiler from moving them across (as wave_lds_sync in
+// gslm_tile.hpp).
+__device__ __forceinline__ void wave_order_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -104,6 +113,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 
 #pragma unroll
   for (int k = 0; k < 4; ++k) s_wcnt[w][lane + 64 * k] = 0u;
+  wave_order_lds();  // the zeroes before any lane's first counter read
   // all loads first (16 keys + 16 values per lane in flight), wave w on keys [wbase, wbase + 1024) of the block
   uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
 #pragma unroll
@@ -137,6 +147,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t cnt = s_wcnt[w][d];
     lrank[r] = cnt + rank;
     if (valid && rank == 0) s_wcnt[w][d] = cnt + (uint32_t)__popcll(m);
+    wave_order_lds();  // this round's counter updates before the next round's reads by other lanes
   }
   __syncthreads();
   // 2. the four waves' offsets inside each digit's run, and each run's block-local start
@@ -204,6 +215,32 @@ __global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ block_s
     carry += tot;
   }
   if (tid == 0) *total = carry;
+}
+
+// In-place form of k_scan_apply (data = in = out, no index gather): one pointer without __restrict__, so the
+// compiler keeps every thread's loads of its elements ahead of its stores to them.
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* data, int64_t n,
+                                                                     const uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    v[k] = i < n ? data[i] : 0u;
+    acc += v[k];
+  }
+  uint32_t tot;
+  const uint32_t inc = block_incl_scan256(acc, s_w, &tot);
+  uint32_t run = block_sums[blockIdx.x] + inc - acc;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) data[i] = run;
+    run += v[k];
+  }
 }
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __restrict__ in,
@@ -375,7 +412,10 @@ int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, i
   const int nb = (int)scan_blocks(n);
   hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, tmp, nb, total);
-  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out);
+  if (out == in && !idx)  // in place (the LM row map's head-flag scan)
+    hipLaunchKernelGGL(k_scan_apply_inplace, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp);
+  else
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GSLM_LIB", os.path.join(os.path.dirname(_HERE), "build", "libgslm.so"))
+_DEFAULT_LIB = os.path.join(os.path.dirname(_HERE), "build", "libgslm.so")
+LIB_PATH = os.environ.get("GSLM_LIB", _DEFAULT_LIB)
 
 GSLM_OK = 0
 GSLM_ERR_INVALID = -1
@@ -190,10 +191,15 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
-    # GSLM_ABI_ANY=1: accept another ABI version whose structs are unchanged (A/B timing of an older build only)
-    if lib.gslm_abi_version() != ABI_VERSION and os.environ.get("GSLM_ABI_ANY") != "1":
-        raise ImportError(f"{LIB_PATH} has C ABI version {lib.gslm_abi_version()}, these bindings need "
-                          f"{ABI_VERSION}: rebuild it")
+    if lib.gslm_abi_version() != ABI_VERSION:
+        # GSLM_ABI_ANY=1 with an explicit GSLM_LIB (the A/B tools timing an older build whose structs are
+        # unchanged): accepted with a warning.  Never for the in-tree product library.
+        if not (os.environ.get("GSLM_ABI_ANY") == "1" and "GSLM_LIB" in os.environ and LIB_PATH != _DEFAULT_LIB):
+            raise ImportError(f"{LIB_PATH} has C ABI version {lib.gslm_abi_version()}, these bindings need "
+                              f"{ABI_VERSION}: rebuild it")
+        import warnings
+        warnings.warn(f"gslm: GSLM_ABI_ANY=1 loads {LIB_PATH} (ABI {lib.gslm_abi_version()}) into ABI "
+                      f"{ABI_VERSION} bindings: A/B timing only, struct layouts are not checked", RuntimeWarning)
     return lib
 
 

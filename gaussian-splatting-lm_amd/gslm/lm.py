@@ -188,12 +188,27 @@ class LMProblem:
                 out.zero_()
             e0, e1 = self.layout.offsets["exposure"]
             out[e0:e1].zero_()
-            return out
+            return self._mark_rhs(out)
         if self.layout.rest_projected:
             full = torch.zeros(self.full_layout.numel, dtype=torch.float32, device=self.device)
             self.rhs_full(full)
-            return self.project(full, out)
-        return self.rhs_full(out)
+            return self._mark_rhs(self.project(full, out))
+        return self._mark_rhs(self.rhs_full(out))
+
+    def _mark_rhs(self, out):
+        """Remember the J^T b this problem produced (exposure slice zeroed): cgls_fused may then skip the exposure
+        slice's D v in every product without checking it (exposure_is_zero)."""
+        self._rhs_token = (out.data_ptr(), out._version)
+        return out
+
+    def exposure_is_zero(self, g):
+        """Whether the exposure slice of the right-hand side g is zero, so that every CG iterate's is (J has no
+        exposure column): true without a device read for the rhs() this problem produced and nobody modified
+        since; otherwise checked on the device (one host sync per solve)."""
+        if getattr(self, "_rhs_token", None) == (g.data_ptr(), g._version):
+            return True
+        e0, e1 = self.layout.offsets["exposure"]
+        return not bool(g[e0:e1].any())
 
     def rhs_full(self, out):
         """J^T b through the drop-in gslm_backward, in the reference's layout (full_layout)."""
@@ -540,6 +555,9 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             check(lib.gslm_axpy_dev(na, pend[0], pend[1], 1.0, off(p), off(x), st), "gslm_axpy_dev")
             pend = None
 
+    # the products may leave y's exposure slice (D v there) unwritten only when g's is zero (exposure_zero)
+    ez = {"exposure_zero": True} if (getattr(prob, "supports_exposure_zero", False) and
+                                     prob.exposure_is_zero(g)) else {}
     first = True
     while iter_total < max_iter:
         if first:
@@ -560,9 +578,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             full = None if pre is None else pre + ((x, pend[0], pend[1]) if pend is not None else (None, None, None))
             if full is not None:
                 pend = None
-            # (q was allocated zero and, like every iterate, has zero exposure components: J has no exposure
-            # column and x0 = 0)
-            ez = {"exposure_zero": True} if getattr(prob, "supports_exposure_zero", False) else {}
+            # (q was allocated zero; with g's exposure slice zero every iterate's is: J has no exposure column
+            # and x0 = 0)
             if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
             reduce(DEL)

@@ -106,3 +106,24 @@ def test_simple_knn_module_binds_the_hip_kernel():
         distCUDA2(torch.zeros(8, 3))
     with pytest.raises(ValueError, match=r"\[N, 3\]"):
         distCUDA2(torch.zeros(8, 2))
+
+
+def test_shipped_library_exports_only_declared_entry_points():
+    """The product .so carries no experiment / debug entry points (the round-2 gslm_dbg_* counters lived behind
+    GSLM_EXPERIMENT_* defines that the product build now refuses): every exported gslm_* symbol is one
+    include/gslm.h declares."""
+    import subprocess
+    from gslm import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("gslm_")})
+    assert not [n for n in exported if n.startswith("gslm_dbg")], exported
+    assert set(exported) <= set(_declared()), set(exported) - set(_declared())
+
+
+def test_product_build_refuses_experiment_flags():
+    import subprocess
+    csrc = os.path.join(ROOT, "gaussian-splatting-lm_amd", "csrc")
+    r = subprocess.run(["make", "-n", "-C", csrc, "EXTRA=-DGSLM_EXPERIMENT_SKIP_JVP"], capture_output=True, text=True)
+    assert r.returncode != 0 and "not part of the product build" in (r.stdout + r.stderr)
+    src = open(os.path.join(csrc, "gslm_device.hpp")).read()
+    assert "#error" in src and "GSLM_EXPERIMENT_SKIP_VJP" in src

@@ -159,8 +159,6 @@ def main():
         ts = [e0.elapsed_time(e1) for e0, e1 in evs]
         res["ramp_ms"] = [round(t, 4) for t in ts[:5]] + [round(sum(ts[i:i + 25]) / len(ts[i:i + 25]), 4)
                                                           for i in range(5, len(ts), 25)]
-    # (GSLM_EXPERIMENT_NOSYNC builds: the forwards of this loop reuse the first one's num_rendered, no round trip)
-    os.environ["GSLM_EXP_NOSYNC_ARM"] = "1"
     vr.forward(graw, prob.stream)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -168,7 +166,6 @@ def main():
         vr.forward(graw, prob.stream)
     torch.cuda.synchronize()
     res["forward_ms"] = 1e3 * (time.perf_counter() - t0) / a.reps
-    del os.environ["GSLM_EXP_NOSYNC_ARM"]
     os.makedirs(a.out, exist_ok=True)
     torch.save({"y": y.cpu(), "color": vr.color.cpu(), "jv": jv.cpu(), "image": vr.image.cpu()}, os.path.join(a.out, a.tag + ".pt"))
     print(json.dumps(res), flush=True)
