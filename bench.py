@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-tiles", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--forward-steps", type=int, default=None)
+    ap.add_argument("--val-views", type=int, default=50, help="line-search validation views (train_jvp.py:214-216)")
+    ap.add_argument("--no-side", action="store_true", help="headline + roofline only (profiling runs)")
     return ap.parse_args()
 
 
@@ -155,7 +157,20 @@ def main():
     gt_prob.evaluate()
     for c, vr in zip(cams, gt_prob.views):
         c.original_image = vr.color.clamp(0, 1).clone()
-    del gt_prob, pert
+    del gt_prob
+    # the line search's validation views (train_jvp.py:214-216: 50 cameras), GT from the same perturbed model; each
+    # rank renders the GT of the views its LossEvaluator will hold (lm_step shards them with shard_views)
+    val_all = orbit_cameras(args.val_views, W, H, seed=5) if not args.no_side else []
+    mine_val = shard_views(len(val_all), rank, world_size)
+    for c0 in range(0, len(mine_val), 8):
+        chunk = [val_all[i].to(device) for i in mine_val[c0:c0 + 8]]
+        vp = LMProblem(pert, chunk, bg, device=device)
+        vp.evaluate()
+        for c, vr in zip(chunk, vp.views):
+            c.original_image = vr.color.clamp(0, 1).clone()
+        del vp
+    del pert
+    torch.cuda.empty_cache()
 
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
     # one view per problem (N = 1): the SH-rest group of the CG vectors is carried as its 3 coordinates in
@@ -227,6 +242,13 @@ def main():
                    "note": "CG iteration with the SH-rest group in the reference's layout (3(K-1) floats per Gaussian)"}
         del pf, gf
         torch.cuda.empty_cache()
+
+    # per-rank stage times of the sharded product (GaussianShardedOperator: tangent records for every view, the two
+    # all-to-alls, the tile pass + screen sums of this rank's views, the shard's gather), HIP events around each
+    # stage of a few extra products outside the timed region
+    shard_stages = None
+    if getattr(prob, "exchange", None) == "gaussian" and hasattr(prob, "stage_times"):
+        shard_stages = prob.stage_times(g, reps=max(args.steps, 5))
 
     # ---------------- raster Mpix/s: full forwards (preprocess, sort, binning, blend; includes the
     # num_rendered read-back the upstream forward also does)
@@ -332,24 +354,29 @@ def main():
     del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
 
-    # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
-    # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
-    fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
-    c0_gpu = time_config0_gpu(device) if rank == 0 else None
-
-    # ---------------- BASELINE configs[2] as train_jvp.py runs it: one full LM step (loss, J^T b, CGLS with
-    # 10 iterations and the reference's residual monitor, 7-point line search on the validation view)
-    lm = time_lm_step(model, cams[:1], bg) if world_size == 1 else None
-    # the SSIM residual (disable_ssim=False): CG iteration on the same view(s)
-    ssim = time_ssim_cg(model, cams[:1], bg, steps=args.steps) if world_size == 1 else None
-
-    # first-order path: the fused Adam step at the bench model's size and one train.py
-    # iteration (render, L1 + SSIM loss, backward, densification statistics, Adam) at configs[1]'s size
-    fo = time_first_order(device, W, H, args.s0, P_adam=args.P, sh=args.sh) if rank == 0 else None
+    fb = c0_gpu = lm = lm_tv = ssim = fo = dropin = None
+    if not args.no_side:
+        # ---------------- BASELINE configs[2] / [3] as train_jvp.py runs it, on every rank: one full LM step (loss,
+        # J^T b, CGLS with 10 iterations and the reference's stopping tests, the 7-point line search on the
+        # reference's 50 validation views), sharded over the ranks; and with the training batch as the validation set
+        lm = time_lm_step(model, cams_all, val_all, bg)
+        lm_tv = time_lm_step(model, cams_all, cams_all, bg, reps=1, with_timing=False)
+        # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
+        # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
+        fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
+        c0_gpu = time_config0_gpu(device) if rank == 0 else None
+        # the drop-in operator at the headline size: what an unchanged train_jvp.py pays per matvec / matvec_T /
+        # evaluate_loss (tests/test_jvp_timing.py:71-106 through the reference's call shapes)
+        dropin = time_dropin_solver_ops(model, cams[0], bg) if rank == 0 else None
+        # the SSIM residual (disable_ssim=False): CG iteration on the same view(s)
+        ssim = time_ssim_cg(model, cams[:1], bg, steps=args.steps) if world_size == 1 else None
+        # first-order path: the fused Adam step at the bench model's size and one train.py
+        # iteration (render, L1 + SSIM loss, backward, densification statistics, Adam) at configs[1]'s size
+        fo = time_first_order(device, W, H, args.s0, P_adam=args.P, sh=args.sh) if rank == 0 else None
 
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and not args.no_side:
         from oracle.cpu_baseline import cpu_matvec_rate
         cm = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu")
         cc = orbit_cameras(1, W, H, seed=1)[0]
@@ -407,7 +434,10 @@ def main():
             "cpu_baseline": cpu,
             "raster_fwd_bwd": fb,
             "configs0_gpu": c0_gpu,
+            "dropin_solver_ops": dropin,
+            "sharded_stage_ms": shard_stages,
             "lm_step": lm,
+            "lm_step_val_is_train": lm_tv,
             "ssim_cg": ssim,
             "first_order": fo,
             "cg_full_layout": cg_full,
@@ -556,20 +586,103 @@ def time_ssim_cg(model, cams, bg, steps=10):
             "ms_per_step": 1e3 * t, "view_matvec_per_s": len(cams) / t}
 
 
-def time_lm_step(model, cams, bg, iters=10, reps=2):
-    """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = restart_iter = iters and check_every=True
-    (host-side stopping tests each iteration, as the reference's CGLS); validation view = the batch."""
+def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True):
+    """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = restart_iter = iters and the reference's stopping
+    tests (on the device), the line search over `val_cams`; every rank calls it (the training and validation views
+    are sharded over the ranks inside).  The model is restored after each step, so every rep solves the same
+    problem; the phase breakdown (evaluate + J^T b, CG, line search) comes from one more step with timing=True."""
     from gslm.lm import lm_step
-    lm_step(model, cams, cams, bg, max_iter=iters, restart_iter=iters, check_every=True)  # warm-up
+    saved = [t.detach().clone() for t in model.params()]
+
+    def restore():
+        with torch.no_grad():
+            for t, s0 in zip(model.params(), saved):
+                t.copy_(s0)
+
+    out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters)  # warm-up (workspaces, clocks)
+    restore()
     torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        out = lm_step(model, cams, cams, bg, max_iter=iters, restart_iter=iters, check_every=True)
+        out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters)
+        restore()
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
-    return {"config": f"full LM step, {len(cams)} view(s), CGLS {iters} iterations + 7-point line search "
-                      "(BASELINE configs[2])", "ms": 1e3 * t, "cg_iters": out["cg"]["iters"],
-            "loss_start": out["start_loss"], "loss_final": out["final_val_loss"]}
+    if dist.is_initialized():
+        tt = torch.tensor([t], dtype=torch.float64, device=saved[0].device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    res = {"config": f"full LM step, {len(cams)} training view(s) over {out['ranks']} rank(s), CGLS {iters} iterations "
+                     f"with the reference's stopping tests + 7-point line search on {len(val_cams)} validation "
+                     "view(s) (train_jvp.py:237-279; BASELINE configs[2], configs[3] at 8 GPUs)",
+           "ms": 1e3 * t, "cg_iters": out["cg"]["iters"], "val_views": len(val_cams), "ranks": out["ranks"],
+           "val_renders_per_rank": 7 * -(-len(val_cams) // out["ranks"]),
+           "loss_start": out["start_loss"], "loss_final": out["final_val_loss"], "best_alpha": out["best_alpha"]}
+    if with_timing:
+        o2 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters, timing=True)
+        restore()
+        res["breakdown_ms"] = o2["timing"]
+    return res
+
+
+def time_dropin_solver_ops(model, cam, bg, reps=5):
+    """The drop-in path an unchanged train_jvp.py runs, at the headline size: tests/test_jvp_timing.py:71-106's three
+    timings through the reference's call shapes on this build's diff_gaussian_rasterization (gslm.train.render =
+    gaussian_renderer.render, activations in PyTorch, GaussianRasterizer's autograd Function):
+      matvec    J u: forward-mode AD (GaussianModel.make_dual, solver_functions.py:83-99) through the render and the
+                disable_ssim residual m clamp(R) - gt (batch_training_loss.py:10-17)
+      matvec_T  J^T v: the render again with grad, then the two .backward calls of the [r; r] pair
+                (loss_image_state.py:93-97, solver_functions.py:101-132)
+      forward   evaluate_loss: render + residual + loss_scalar (solver_functions.py:31-53)
+    Median of `reps` host-timed calls, each synchronised (the reference's script does not synchronise)."""
+    import types
+    import torch.autograd.forward_ad as fwAD
+    from gslm.train import PipelineParams, render
+    pipe = PipelineParams()
+    gt = cam.original_image
+    m = cam.alpha_mask
+    g3 = torch.Generator().manual_seed(3)
+    u = types.SimpleNamespace(**{f"{k}_grad": torch.randn(t.shape, generator=g3).to(t.device) for k, t in
+                                 zip(("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity", "exposure"),
+                                     model.params())})
+    v = torch.randn(gt.shape, generator=torch.Generator().manual_seed(4)).to(gt.device)
+
+    def residual():
+        img = render(cam, model, pipe, bg.to(gt.device))["render"]
+        return img * m - gt if m is not None else img - gt
+
+    def matvec():
+        with torch.no_grad(), fwAD.dual_level(), model.make_dual(u):
+            return fwAD.unpack_dual(residual()).tangent
+
+    def matvec_T():
+        model.zero_grad()
+        r = residual()
+        r.backward(v, retain_graph=True)  # the L1 slot
+        r.backward(v)                     # the aliased "ssim" slot
+        return model._opacity.grad
+
+    def forward():
+        with torch.no_grad():
+            r = residual()
+            return 2.0 * (r.double() ** 2).sum()
+
+    out = {"config": f"{model._xyz.shape[0]} Gaussians SH{model.active_sh_degree}, 1x{cam.image_width}x"
+                     f"{cam.image_height} view, drop-in rasterizer through render() (tests/test_jvp_timing.py:71-106)"}
+    for name, fn in (("matvec", matvec), ("matvec_T", matvec_T), ("forward", forward)):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        out[name + "_ms"] = 1e3 * sorted(ts)[len(ts) // 2]
+    model.zero_grad()
+    return out
 
 
 def time_drop_in_fwd_bwd(device, W, H, s0, P=100_000, sh=3, reps=10):

@@ -197,6 +197,29 @@ int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
   return GSLM_OK;
 }
 
+int gslm_num_rendered_many(const void* const* geoms, const int64_t* Ps, int32_t n, int64_t* out, void* stream) {
+  if (n < 0 || (n > 0 && (!geoms || !Ps || !out))) { set_error("num_rendered_many: NULL argument"); return GSLM_ERR_INVALID; }
+  if (n == 0) return GSLM_OK;
+  // one pinned array per host thread, grown on demand: n small copies, then ONE stream sync
+  thread_local uint32_t* pinned = nullptr;
+  thread_local int32_t cap = 0;
+  if (cap < n) {
+    if (pinned) GSLM_HIP_CHECK(hipHostFree(pinned));
+    pinned = nullptr;
+    cap = 0;
+    GSLM_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t) * (size_t)n, hipHostMallocDefault));
+    cap = n;
+  }
+  for (int32_t k = 0; k < n; ++k) {
+    GeomBufs gb;
+    geom_layout(Ps[k], const_cast<void*>(geoms[k]), &gb);
+    GSLM_HIP_CHECK(hipMemcpyAsync(pinned + k, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  }
+  GSLM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  for (int32_t k = 0; k < n; ++k) out[k] = (int64_t)pinned[k];
+  return GSLM_OK;
+}
+
 int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
                    int64_t N, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
                    void* stream) {
@@ -382,6 +405,7 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   }
   if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
+  b.v.stop = opts ? opts->cg_ctl : nullptr;
   const bool proj = opts && (opts->flags & GSLM_MV_SH_REST_PROJECTED) && b.g.M > 1;
   GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
   if (proj) {

@@ -94,13 +94,17 @@ __global__ __launch_bounds__(256) void k_xpby_dev(int64_t n, const float* __rest
 // MONITOR also accumulates <x_new, g> and <x_new, s_new> (partials at part + nb, part + 2 nb): the
 // residual monitor of conjugate_gradient.py:103-104, b^2 - <x, J^T b> - <x, s>, without two more
 // passes over x.
+// ctl (or NULL): the device CG control block of k_cg_monitor -- a stopped solve, or delta < 1e-20 (the
+// reference's early termination, conjugate_gradient.py:88-91, before x moves), leaves x and s untouched.
 template <bool MONITOR>
 __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const double* __restrict__ gam,
                                                            const double* __restrict__ del,
                                                            const float* __restrict__ p, const float* __restrict__ q,
                                                            float* __restrict__ x, float* __restrict__ s,
-                                                           const float* __restrict__ g, double* __restrict__ part) {
+                                                           const float* __restrict__ g, double* __restrict__ part,
+                                                           const double* __restrict__ ctl) {
   __shared__ double sm[DOT_THREADS / 64];
+  if (ctl && (ctl[0] != 0.0 || *del < 1e-20)) return;
   const float a = (float)((*gam) / (*del));
   double acc = 0.0, axg = 0.0, axs = 0.0;
   const int64_t n4 = n / 4;
@@ -156,6 +160,39 @@ __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const doub
   }
 }
 
+// The stopping tests of conjugate_gradient.py:88-117 on the device, once per inner iteration after the update
+// (and the cross-rank sums of its scalars): ctl = [stop, iters, last_res, n_hist, history...] (doubles).
+//   delta < 1e-20                       -> stop = 1 (x not moved: k_cg_update skipped it)
+//   res = b^2 - <x, g> - <x, s> (the residual monitor of :103-104) appended to the history;
+//   res > last_res                      -> stop = 2 (after the step, as the reference breaks after x += alpha p)
+//   gamma' < max(tol sqrt(gamma), atol) -> stop = 3
+//   otherwise iters += 1 (iter_total).  A stopped solve's later kernels return at once (ViewK::stop, k_cg_update).
+// Same double arithmetic as the host-side tests of gslm.lm.cgls_fused.
+__global__ void k_cg_monitor(const double* __restrict__ gam, const double* __restrict__ gamn,
+                             const double* __restrict__ del, const double* __restrict__ xg,
+                             const double* __restrict__ xs, const double* __restrict__ b2, double tol, double atol,
+                             double* __restrict__ ctl, int max_hist) {
+  if (threadIdx.x != 0 || ctl[0] != 0.0) return;
+  if (*del < 1e-20) {
+    ctl[0] = 1.0;
+    return;
+  }
+  const double res = (*b2 - *xg) - *xs;
+  const int nh = (int)ctl[3];
+  if (nh < max_hist) ctl[4 + nh] = res;
+  ctl[3] = (double)(nh + 1);
+  if (res > ctl[2]) {
+    ctl[0] = 2.0;
+    return;
+  }
+  ctl[2] = res;
+  if (*gamn < fmax(tol * sqrt(*gam), atol)) {
+    ctl[0] = 3.0;
+    return;
+  }
+  ctl[1] += 1.0;
+}
+
 __global__ __launch_bounds__(256) void k_damp_add(int64_t n, const float* __restrict__ x, Groups g,
                                                   float* __restrict__ y) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -201,7 +238,7 @@ int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, cons
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_cg_update<false>, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s,
-                     nullptr, (double*)scratch);
+                     nullptr, (double*)scratch, (const double*)nullptr);
   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, (const double*)scratch, DOT_BLOCKS, gam_new_dev);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
@@ -209,7 +246,7 @@ int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, cons
 
 int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                            float* x, float* s, const float* g, void* scratch, size_t scratch_bytes,
-                           double* gam_new_dev, double* xg_dev, double* xs_dev, void* stream) {
+                           double* gam_new_dev, double* xg_dev, double* xs_dev, const double* cg_ctl, void* stream) {
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(x) |
        reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(g)) & 15) {
     set_error("gslm_cg_update_monitor: vectors must be 16-byte aligned");
@@ -222,10 +259,23 @@ int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_d
   hipStream_t st = (hipStream_t)stream;
   const double* part = (const double*)scratch;
   hipLaunchKernelGGL(k_cg_update<true>, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s, g,
-                     (double*)scratch);
+                     (double*)scratch, cg_ctl);
   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part, DOT_BLOCKS, gam_new_dev);
   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + DOT_BLOCKS, DOT_BLOCKS, xg_dev);
   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + 2 * DOT_BLOCKS, DOT_BLOCKS, xs_dev);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int gslm_cg_monitor(const double* gam_dev, const double* gam_new_dev, const double* del_dev, const double* xg_dev,
+                    const double* xs_dev, const double* b2_dev, double tol, double atol, double* cg_ctl,
+                    int32_t max_hist, void* stream) {
+  if (!gam_dev || !gam_new_dev || !del_dev || !xg_dev || !xs_dev || !b2_dev || !cg_ctl || max_hist < 0) {
+    set_error("gslm_cg_monitor: NULL scalar / control block or negative max_hist");
+    return GSLM_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(k_cg_monitor, dim3(1), dim3(64), 0, (hipStream_t)stream, gam_dev, gam_new_dev, del_dev, xg_dev,
+                     xs_dev, b2_dev, tol, atol, cg_ctl, max_hist);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256, PROJ ? 5 : 1) void k_gather_lm(ViewK v, GaussK
                                                     const uint32_t* __restrict__ hscan,
                                                     const float4* __restrict__ rows, FlatK o) {
   o.rest_proj = PROJ ? 1 : 0;  // the launcher picked the variant from it
+  if (cg_stopped(v)) return;
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // row chunks, then the factored SH stage
   __shared__ double s_dot[4];
   const int tid = threadIdx.x;

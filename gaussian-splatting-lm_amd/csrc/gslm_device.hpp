@@ -46,7 +46,13 @@ struct ViewK {
   int M;                                 // SH coefficients stored per Gaussian
   int antialiasing;
   int exhaustive;                        // gslm_view.debug: disable the quadrant cull (reference traversal)
+  // gslm_matvec_opts.cg_ctl: the device CG control block; a product kernel of a stopped solve (stop[0] != 0)
+  // returns at once (cgls_fused's device-side stopping tests; NULL outside the CG loop)
+  const double* stop = nullptr;
 };
+
+// block-uniform early exit of a product kernel once the device-side CG stopping tests fired
+__device__ __forceinline__ bool cg_stopped(const ViewK& v) { return v.stop != nullptr && *v.stop != 0.0; }
 
 // transformPoint4x3 / 4x4, one row at a time (same association as the oracle)
 __device__ __forceinline__ float tp_row(const float* m, float x, float y, float z, int r) {

@@ -289,6 +289,7 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
   float4* s_t0 = s_lds;  // jvp_tile's tangent records (WITH_XY), below s_r0
   float4* s_t1 = s_t0 + B;
   float2* s_t2 = reinterpret_cast<float2*>(s_t1 + B);
+  if (cg_stopped(v)) return;
   const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
   const int tid = threadIdx.x;

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_lm_residual(int64_t HW, const f
       const float inside = (R >= 0.0f && R <= 1.0f) ? 1.0f : 0.0f;
       const float r = m * fminf(fmaxf(R, 0.0f), 1.0f) - gt[k];
       if (residual) residual[k] = r;
-      weight[k] = (m * m) * inside;
+      if (weight) weight[k] = (m * m) * inside;
       if (seed) seed[k] = ((-2.0f * m) * inside) * r;
       acc += (double)r * (double)r;
     }
@@ -85,7 +85,7 @@ int gslm_lm_residual(int32_t H, int32_t W, const float* color, const float* gt, 
                      double* loss_dev, int32_t accumulate, void* stream) {
   if (H < 0 || W < 0) { set_error("lm_residual: negative image size"); return GSLM_ERR_INVALID; }
   const int64_t HW = (int64_t)H * W;
-  if (HW > 0 && (!color || !gt || !weight)) { set_error("lm_residual: NULL color / gt / weight"); return GSLM_ERR_INVALID; }
+  if (HW > 0 && (!color || !gt)) { set_error("lm_residual: NULL color / gt"); return GSLM_ERR_INVALID; }
   if (!loss_dev || !scratch) { set_error("lm_residual: NULL loss or scratch"); return GSLM_ERR_INVALID; }
   if (scratch_bytes < gslm_residual_scratch_bytes(H, W)) { set_error("lm_residual: scratch too small"); return GSLM_ERR_CAPACITY; }
   hipStream_t s = (hipStream_t)stream;

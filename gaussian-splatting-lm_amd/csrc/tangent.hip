@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, Gauss
                                                          const uint32_t* __restrict__ tiles,
                                                          float4* __restrict__ trec, XpbyK xp, int compact) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
+  if (cg_stopped(v)) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (XPBY) {
     // the direction this kernel reads is the updated one: each thread reads back only its own

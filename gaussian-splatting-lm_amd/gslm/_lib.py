@@ -61,6 +61,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("screen_out", ctypes.c_void_p), ("pixel_seed", ctypes.c_void_p), ("jv_out", ctypes.c_void_p),
         ("alpha_num", ctypes.c_void_p), ("alpha_den", ctypes.c_void_p), ("xpby_x_offset", ctypes.c_int64),
         ("trec_in", ctypes.c_void_p), ("screen_stride", ctypes.c_int64),
+        ("cg_ctl", ctypes.c_void_p),
     ]
 
 
@@ -85,6 +86,8 @@ EXPORTS = {
                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_num_rendered": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                          ctypes.c_void_p]),
+    "gslm_num_rendered_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                              ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -126,7 +129,10 @@ EXPORTS = {
     "gslm_cg_update_monitor": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
-                                              ctypes.c_void_p, ctypes.c_void_p]),
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_cg_monitor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "gslm_dot_finalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_dot_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gslm_dot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
@@ -175,7 +181,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 4  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 5  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):

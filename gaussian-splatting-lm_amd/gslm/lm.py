@@ -270,30 +270,33 @@ class LMProblem:
         vec[o["exposure"][0]:o["exposure"][1]].zero_()
 
     # -------------------------------------------------------------- (J^T J + D) v
-    def matvec(self, v, y):
+    def matvec(self, v, y, cg_ctl=None):
         """y = sum_b 2 J_b^T W_b J_b v + D v (fused per view; D v folded into the first view's gather)."""
-        self.matvec_dot(v, y, None)
+        self.matvec_dot(v, y, None, cg_ctl=cg_ctl)
         return y
 
-    # cgls_fused may pass exposure_zero=True (see matvec_dot)
+    # cgls_fused may pass exposure_zero=True (see matvec_dot) and the device CG control block (cg_ctl)
     supports_exposure_zero = True
+    supports_cg_ctl = True
 
-    def matvec_dot(self, v, y, dot_out, pre=None, exposure_zero=False):
+    def matvec_dot(self, v, y, dot_out, pre=None, exposure_zero=False, cg_ctl=None):
         """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
         view; exposure components of v zero, as in every LM iterate).  Returns True if fused.
         pre = (s, beta_num_ptr, beta_den_ptr): first v <- s + beta v (the deferred CG direction
         update), fused into the first view's tangent kernel.
         exposure_zero: the caller guarantees that the exposure components of v (after pre) and of y are
         zero already -- true of every CG iterate (J has no exposure column, x0 = 0, y is the solver's own
-        q) -- so y's exposure slice D v = 0 is left as it is (no elementwise launch per product)."""
+        q) -- so y's exposure slice D v = 0 is left as it is (no elementwise launch per product).
+        cg_ctl: device pointer of cgls_fused's CG control block (gslm_cg_monitor): once its stopping tests
+        have fired the product's kernels return at once (gslm_matvec_opts.cg_ctl)."""
         fuse = dot_out is not None and len(self.views) == 1
         self.local_normal_matvec(v, y, damp=True, dot_out=dot_out if fuse else None, pre=pre,
-                                 exposure_zero=exposure_zero)
+                                 exposure_zero=exposure_zero, cg_ctl=cg_ctl)
         return fuse
 
-    def local_normal_matvec(self, v, y, damp=False, dot_out=None, pre=None, exposure_zero=False):
+    def local_normal_matvec(self, v, y, damp=False, dot_out=None, pre=None, exposure_zero=False, cg_ctl=None):
         """y = [D v +] sum over this problem's views of 2 J_b^T W_b J_b v  (overwrites y).
-        pre, exposure_zero: see matvec_dot."""
+        pre, exposure_zero, cg_ctl: see matvec_dot."""
         g = raw_gaussians(self.model)
         vs = self.layout.grads_struct(v)
         ys = self.layout.grads_struct(y)
@@ -312,6 +315,7 @@ class LMProblem:
             opts.stages = STAGE_ALL | (STAGE_OVERWRITE if b == 0 else 0)
             opts.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
             opts.damp7 = self._damps if (damp and b == 0) else None
+            opts.cg_ctl = cg_ctl
             if pre is not None and b == 0:
                 ss = self._pre_opts(opts, v, pre)  # noqa: F841  (kept alive for the call)
             if dot_out is not None and b == last:
@@ -372,6 +376,7 @@ class LMProblem:
         o1.xpby_s, o1.beta_num, o1.beta_den = opts.xpby_s, opts.beta_num, opts.beta_den
         o1.xpby_tail_v, o1.xpby_tail_s, o1.xpby_tail_n = opts.xpby_tail_v, opts.xpby_tail_s, opts.xpby_tail_n
         o1.alpha_num, o1.alpha_den, o1.xpby_x_offset = opts.alpha_num, opts.alpha_den, opts.xpby_x_offset
+        o1.cg_ctl = opts.cg_ctl
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs), jv.data_ptr(), 1,
                                       vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                       vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o1),
@@ -384,6 +389,7 @@ class LMProblem:
         o2.pixel_seed = u.data_ptr()
         o2.damp7 = opts.damp7
         o2.dot_vy, o2.dot_scratch, o2.dot_scratch_bytes = opts.dot_vy, opts.dot_scratch, opts.dot_scratch_bytes
+        o2.cg_ctl = opts.cg_ctl
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs), u.data_ptr(), 1,
                                       vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                       vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o2),
@@ -514,12 +520,16 @@ class LMProblem:
 
 
 def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check_every=True, verbose=False,
-               callback=None):
+               callback=None, host_checks=None):
     """cgls_damped (conjugate_gradient.py:51-127) on the fused operator, x0 = 0.
 
-    Returns (x, info).  With check_every=False the stopping tests are skipped and no iteration
-    synchronises with the host (benchmark mode); the iterates are identical either way while no
-    test fires."""
+    Returns (x, info).  check_every: the reference's stopping tests (delta < 1e-20, residual increase, gamma
+    tolerance).  They run on the device by default (gslm_cg_monitor: a control block the update and product
+    kernels test, one read-back at the end, no host synchronisation inside the loop -- the host enqueues the
+    whole max_iter x restart_iter schedule and a stopped solve's remaining launches return at once);
+    host_checks=True (or verbose / a callback, which need the values each iteration) reads the scalars back
+    every iteration instead.  Both give the same iterates, stop and history.  With check_every=False the tests
+    are skipped (benchmark mode); the iterates are identical while no test fires."""
     n = prob.layout.numel
     dev = prob.device
     st = prob.stream
@@ -535,7 +545,20 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     s = torch.empty_like(x)
     p = torch.empty_like(x)
     q = torch.zeros_like(x)
-    b2 = float(prob.loss) if check_every else None  # ||b||^2 = loss
+    if host_checks is None:
+        host_checks = verbose or callback is not None
+    on_device = check_every and not host_checks
+    ctl = None
+    if on_device:
+        # [stop, iters, last_res, n_hist, history...] (gslm_cg_monitor)
+        ctl = torch.full((4 + max_iter,), math.nan, dtype=torch.float64, device=dev)
+        ctl[:4] = torch.tensor([0.0, 0.0, math.inf, 0.0], dtype=torch.float64)
+        loss = prob.loss
+        b2_dev = loss if (torch.is_tensor(loss) and loss.is_cuda and loss.dtype == torch.float64 and
+                          loss.numel() == 1) else torch.tensor(float(loss), dtype=torch.float64, device=dev)
+    cg_ctl = ctl.data_ptr() if ctl is not None else None
+    ctl_kw = {"cg_ctl": cg_ctl} if (cg_ctl is not None and getattr(prob, "supports_cg_ctl", False)) else {}
+    b2 = float(prob.loss) if (check_every and not on_device) else None  # ||b||^2 = loss
     iter_total, last_res, history = 0, math.inf, []
     # Benchmark mode defers x += alpha p into the next product's xpby pass (gslm_matvec_opts.alpha_num):
     # the update kernel then streams s and q only; the iterates are bitwise those of the undeferred loop.
@@ -565,7 +588,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             first = False
         else:
             flush()
-            prob.matvec(x, q)
+            prob.matvec(x, q, **ctl_kw)
             torch.sub(g, q, out=s)
         p.copy_(s)
         prob.dot(s[lo:], s[lo:], ptr(GAM))
@@ -580,10 +603,10 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 pend = None
             # (q was allocated zero; with g's exposure slice zero every iterate's is: J has no exposure column
             # and x0 = 0)
-            if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez):
+            if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez, **ctl_kw):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
             reduce(DEL)
-            if check_every and sc[DEL].item() < 1e-20:
+            if check_every and not on_device and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
                 stop = True
@@ -592,8 +615,11 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             if check_every:
                 check(lib.gslm_cg_update_monitor(na, ptr(GAM), ptr(DEL), off(p), off(q), off(x), off(s), off(g),
                                                  prob.dot_scratch.data_ptr(), prob.dot_scratch.numel() * 8,
-                                                 ptr(GAMN), ptr(XG), ptr(XS), st))
+                                                 ptr(GAMN), ptr(XG), ptr(XS), cg_ctl, st))
                 reduce(GAMN, XG, XS)
+                if on_device:  # the stopping tests of :88-117 on the device (gslm_cg_monitor)
+                    check(lib.gslm_cg_monitor(ptr(GAM), ptr(GAMN), ptr(DEL), ptr(XG), ptr(XS), b2_dev.data_ptr(),
+                                              float(tol), float(atol), cg_ctl, max_iter, st), "gslm_cg_monitor")
             elif defer:
                 check(lib.gslm_cg_update(na, ptr(GAM), ptr(DEL), off(p), off(q), None, off(s),
                                          prob.dot_scratch.data_ptr(), ptr(GAMN), st))
@@ -605,7 +631,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 reduce(GAMN)
             # beta = gamma' / gamma; after the slot swap below these are the GAM / GAMN slots
             pre = (s, ptr(GAMN), ptr(GAM))
-            if check_every:
+            if check_every and not on_device:
                 vals = sc[:5].tolist()
                 res = b2 - vals[XG] - vals[XS]  # ||b - J x||^2 + x^T D x  (monitor of conjugate_gradient.py:103-104)
                 history.append(res)
@@ -628,6 +654,11 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
         if stop:
             break
     flush()
+    if on_device:
+        c = ctl.tolist()  # the solve's one read-back
+        iter_total, nh = int(c[1]), int(c[3])
+        history = c[4:4 + min(nh, max_iter)]
+        return x, {"iters": iter_total, "residuals": history, "stop": int(c[0])}
     return x, {"iters": iter_total, "residuals": history}
 
 
@@ -708,6 +739,82 @@ def cgls_residual(prob, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, verbo
     return x, {"iters": iter_total, "residuals": history}
 
 
+class LossEvaluator:
+    """The line search's validation loss: `val_loss_func().loss_scalar` of train_jvp.py:258,268,279 (batch_training_loss
+    with disable_ssim=True over the validation views: 2 sum_b ||m_b clamp01(R_b) - gt_b||^2) on the HIP forward.
+
+    Per view: gslm_preprocess -> gslm_rasterize -> gslm_lm_residual in its loss-only form (no residual, weight or
+    seed images).  Views run in batches of `batch` workspaces: a batch's preprocesses are enqueued first and one
+    gslm_num_rendered_many read-back sizes all their binnings (one host round trip per batch, not per view); the
+    loss accumulates in a device double, in view order.  `reduce`: a callable summing the device double over the
+    ranks that hold the other views (the multi-GPU line search, gslm.parallel.allreduce_loss)."""
+
+    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None):
+        self.model = model
+        self.device = device
+        self.reduce = reduce
+        self.gts = [c.original_image.to(device) for c in cams] if gts is None else gts
+        ms = [c.alpha_mask for c in cams] if alpha_masks is None else alpha_masks
+        self.masks = [None if m is None else m.to(device=device, dtype=torch.float32).contiguous() for m in ms]
+        self.views = [_lib.view_from_camera(c, bg, model.active_sh_degree) for c in cams]
+        for vw, gt, m in zip(self.views, self.gts, self.masks):
+            H, W = vw.image_height, vw.image_width
+            if gt.shape != (3, H, W) or gt.dtype != torch.float32:
+                raise ValueError(f"ground truth must be float32 (3, {H}, {W}), got {gt.dtype} {tuple(gt.shape)}")
+            if m is not None and m.numel() != H * W:
+                raise ValueError("alpha mask must be [1, H, W]")
+        self.stream = _lib.stream_handle(device)
+        self.batch = max(1, min(int(batch), len(cams) or 1))
+        self.slots = [dict(geom=None, binning=None, image=None, color=None) for _ in range(self.batch)]
+        self.res_scratch = torch.empty(lib.gslm_residual_scratch_bytes(1, 1) // 8, dtype=torch.float64,
+                                       device=device)
+        self.num_rendered = [0] * len(cams)
+
+    def _slot(self, k, P, H, W):
+        sl = self.slots[k]
+        if sl["geom"] is None or sl["geom"].numel() < lib.gslm_geom_bytes(P):
+            sl["geom"] = _lib.u8(lib.gslm_geom_bytes(P), self.device)
+        if sl["image"] is None or sl["image"].numel() < lib.gslm_image_bytes(H, W):
+            sl["image"] = _lib.u8(lib.gslm_image_bytes(H, W), self.device)
+            sl["color"] = torch.empty(3 * H * W, dtype=torch.float32, device=self.device)
+        return sl
+
+    def evaluate(self):
+        """Device double: the loss over this evaluator's views (summed over the ranks with `reduce`)."""
+        g = raw_gaussians(self.model)
+        P = g.P
+        loss = torch.zeros((), dtype=torch.float64, device=self.device)
+        V = len(self.views)
+        for b0 in range(0, V, self.batch):
+            idx = list(range(b0, min(V, b0 + self.batch)))
+            slots = [self._slot(k, P, self.views[i].image_height, self.views[i].image_width) for k, i in enumerate(idx)]
+            for sl, i in zip(slots, idx):
+                check(lib.gslm_preprocess(ctypes.byref(self.views[i]), ctypes.byref(g), sl["geom"].data_ptr(),
+                                          sl["geom"].numel(), None, self.stream), "gslm_preprocess")
+            geoms = (ctypes.c_void_p * len(idx))(*[sl["geom"].data_ptr() for sl in slots])
+            Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
+            Ns = (ctypes.c_int64 * len(idx))()
+            check(lib.gslm_num_rendered_many(geoms, Ps, len(idx), Ns, self.stream), "gslm_num_rendered_many")
+            for k, (sl, i) in enumerate(zip(slots, idx)):
+                vw = self.views[i]
+                H, W, N = vw.image_height, vw.image_width, int(Ns[k])
+                self.num_rendered[i] = N
+                need = lib.gslm_binning_bytes(N, H, W)
+                if sl["binning"] is None or sl["binning"].numel() < need:
+                    sl["binning"] = _lib.u8(int(need * 1.25) + 4096, self.device)
+                check(lib.gslm_rasterize(ctypes.byref(vw), P, sl["geom"].data_ptr(), sl["binning"].data_ptr(),
+                                         sl["binning"].numel(), N, sl["image"].data_ptr(), sl["image"].numel(),
+                                         sl["color"].data_ptr(), None, self.stream), "gslm_rasterize")
+                m = self.masks[i]
+                check(lib.gslm_lm_residual(H, W, sl["color"].data_ptr(), self.gts[i].data_ptr(),
+                                           None if m is None else m.data_ptr(), None, None, None,
+                                           self.res_scratch.data_ptr(), self.res_scratch.numel() * 8,
+                                           loss.data_ptr(), int(i > 0), self.stream), "gslm_lm_residual")
+        if self.reduce is not None:
+            self.reduce(loss)
+        return loss
+
+
 def update_params(model, layout, step, scale):
     """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step."""
     v = layout.views(step)
@@ -722,38 +829,85 @@ def update_params(model, layout, step, scale):
 
 
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
-            verbose=False, device="cuda", sh_projection="auto", recursion="fused"):
+            verbose=False, device="cuda", sh_projection="auto", recursion="fused", exchange="auto", group=None,
+            val_batch=8, timing=False, backend=None):
     """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search.
-    With one training view the SH-rest group of the CG vectors is carried projected (LMProblem).
+
+    Single process: LMProblem over `cams` (with one training view the SH-rest group of the CG vectors is carried
+    projected).  Under torch.distributed (several ranks, or GSLM_FORCE_COLLECTIVES=1 at one rank) the step runs
+    sharded, every rank calling lm_step with the same arguments: the training views are split over the ranks
+    (gslm.parallel.ShardedLMProblem -- Gaussian-sharded CG vectors when every rank holds as many views, else the
+    replicated-vector exchanges), the step is gathered whole on every rank (gather_full), the validation views are
+    split the same way and each line-search loss is one 8-byte all-reduce, and every rank applies the identical
+    update_step -- the replicas stay bitwise equal.
     recursion: "fused" (cgls_fused, one fused (J^T J + D) p per iteration) or "cgls" (cgls_residual, the
-    reference's residual-space recursion)."""
-    prob = LMProblem(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device, sh_projection=sh_projection)
+    reference's residual-space recursion; single process only).  check_every: the reference's stopping tests,
+    on the device (cgls_fused).  timing=True adds wall-clock phases (evaluate + J^T b, CG, line search) to the
+    result, synchronising the device at their boundaries.
+    backend: (problem_cls, evaluator_cls, solver) replacing (LMProblem, LossEvaluator, cgls_fused) -- the CPU
+    multi-process tests run this same driver, sharding and reductions on the oracle restatement."""
+    import time
+    from gslm.parallel import ShardedLMProblem, allreduce_loss, collectives_on, shard_views, world
+    rank, n = world()
+    sharded = collectives_on(n)
+    problem_cls, evaluator_cls, solver = backend if backend is not None else (LMProblem, LossEvaluator, cgls_fused)
+    t = {}
+    clock = [time.perf_counter()]
+
+    def lap(name):
+        if timing:
+            if torch.device(device).type == "cuda":
+                torch.cuda.synchronize(device)
+            now = time.perf_counter()
+            t[name] = 1e3 * (now - clock[0])
+            clock[0] = now
+
+    if sharded:
+        if recursion != "fused":
+            raise ValueError("the sharded LM step runs cgls_fused")
+        mine = [cams[i] for i in shard_views(len(cams), rank, n)]
+        prob = ShardedLMProblem(model, mine, bg, group=group, all_cams=cams, exchange=exchange, mask_xyz=mask_xyz,
+                                damp=damp, device=device, problem_cls=problem_cls)
+    else:
+        prob = problem_cls(model, cams, bg, mask_xyz=mask_xyz, damp=damp, device=device, sh_projection=sh_projection)
     start_loss = prob.evaluate()
     if recursion == "cgls":
+        lap("evaluate_rhs_ms")
         s, info = cgls_residual(prob, max_iter=max_iter, restart_iter=restart_iter, verbose=verbose)
     elif recursion == "fused":
         g = prob.rhs(prob.zeros())
-        s, info = cgls_fused(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
-                             verbose=verbose)
+        lap("evaluate_rhs_ms")
+        s, info = solver(prob, g, max_iter=max_iter, restart_iter=restart_iter, check_every=check_every,
+                         verbose=verbose)
     else:
         raise ValueError(f"recursion must be 'fused' or 'cgls', got {recursion!r}")
-    s = prob.expand(s)
+    # the whole step in the reference's layout, identical on every rank
+    s = prob.gather_full(s) if getattr(prob, "exchange", None) == "gaussian" else getattr(prob, "expand", lambda v: v)(s)
+    start_loss = float(start_loss)
     del prob
-    val = LMProblem(model, val_cams, bg, mask_xyz=mask_xyz, damp=damp, device=device)
+    lap("cg_ms")
+    full = ParamLayout(model._xyz.shape[0], 1 + model._features_rest.shape[1], model._exposure.shape[0])
+    mine_val = [val_cams[i] for i in shard_views(len(val_cams), rank, n)] if sharded else val_cams
+    val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
+                        reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
     # train_jvp.py:262-279: alpha = 2, 1, ..., 1/16 on the validation views, keep the best, step to it
     alpha = 2.0
     best_alpha, best_loss = alpha, math.inf
     trace = []
-    update_params(model, val.full_layout, s, alpha)
+    update_params(model, full, s, alpha)
     for _ in range(6):
         vl = float(val.evaluate())
         trace.append((alpha, vl))
         if vl < best_loss:
             best_loss, best_alpha = vl, alpha
         new_alpha = alpha * 0.5
-        update_params(model, val.full_layout, s, new_alpha - alpha)
+        update_params(model, full, s, new_alpha - alpha)
         alpha = new_alpha
-    update_params(model, val.full_layout, s, best_alpha - alpha)
+    update_params(model, full, s, best_alpha - alpha)
     final = float(val.evaluate())
-    return dict(start_loss=float(start_loss), final_val_loss=final, best_alpha=best_alpha, cg=info, step=s,
-                trace=trace)
+    lap("line_search_ms")
+    out = dict(start_loss=start_loss, final_val_loss=final, best_alpha=best_alpha, cg=info, step=s, trace=trace,
+               val_views=len(val_cams), ranks=n if sharded else 1)
+    if timing:
+        out["timing"] = t
+    return out

@@ -42,6 +42,15 @@ def collectives_on(world_size):
     return world_size > 1 or os.environ.get("GSLM_FORCE_COLLECTIVES") == "1"
 
 
+def allreduce_loss(t, group=None):
+    """Sum a device (or host) double over the ranks in place: the multi-GPU line search's validation loss, one
+    8-byte all-reduce per evaluation (every rank gets the bitwise same sum, so every rank takes the same
+    line-search decisions)."""
+    if collectives_on(world()[1]):
+        _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group), t.view(1))
+    return t
+
+
 def shard_views(n_views, rank, world_size):
     """Contiguous block of view indices owned by `rank` (weak scaling: equal blocks)."""
     per = (n_views + world_size - 1) // world_size
@@ -154,21 +163,23 @@ class ShardedOperator:
         return y
 
 
-def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto", **kw):
+def ShardedLMProblem(model, cams, bg, group=None, all_cams=None, exchange="auto", problem_cls=None, **kw):
     """LMProblem over this rank's views, wrapped for the cross-rank reductions.  all_cams (every
-    rank's views, in rank order) enables the screen and Gaussian-sharded exchanges.
+    rank's views, in rank order) enables the screen and Gaussian-sharded exchanges.  problem_cls: the per-rank
+    problem (gslm.lm.LMProblem; the CPU tests pass oracle.lm_ref.OracleLMProblem).
 
     exchange: "gaussian" (GaussianShardedOperator: CG vectors sharded by Gaussian, two all-to-alls per
     product), "screen" / "allreduce" (ShardedOperator: vectors replicated), or "auto" -- "gaussian" when
     several ranks render the same number of views each with the disable_ssim residual, else
     ShardedOperator's own choice."""
-    from gslm.lm import LMProblem
+    if problem_cls is None:
+        from gslm.lm import LMProblem as problem_cls
     rank, n = world()
     if n > 1 or (all_cams is not None and len(all_cams) > 1) or exchange == "gaussian":
         # the SH-rest span is one view's: the global batch has several (and the Gaussian-sharded exchange
         # runs on the full layout)
         kw["sh_projection"] = False
-    local = LMProblem(model, cams, bg, **kw)
+    local = problem_cls(model, cams, bg, **kw)
     if exchange == "auto" and n > 1 and all_cams is not None and len(cams) >= 1 and \
             len(all_cams) == n * len(cams) and local.mask_xyz and not local.ssim:
         exchange = "gaussian"
@@ -252,6 +263,7 @@ class GaussianShardedOperator:
             self._bufs = None
         if hasattr(local, "_damps"):
             self._damps = local._damps
+        self._events = None  # stage_times: HIP events recorded between the product's stages
 
     def __getattr__(self, name):  # stream, dot_scratch, views, weights, model, ...
         return getattr(self.local, name)
@@ -436,10 +448,32 @@ class GaussianShardedOperator:
             opts.xpby_x_offset = x.data_ptr() - v.data_ptr()
         return ss
 
+    STAGES = ("tangent_views", "all_to_all_trec", "render_screen", "all_to_all_screen", "gather_screen")
+
+    def stage_times(self, v, reps=10):
+        """Per-stage time of this rank's product (ms, mean over `reps` products of direction v): HIP events on the
+        product's stream between the five stages of _matvec_kernels (the all-to-alls include their wait)."""
+        y = self.zeros()
+        evs = []
+        for _ in range(reps):
+            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.STAGES) + 1)]
+            self.matvec_dot(v, y, None)
+            evs.append(self._events)
+            self._events = None
+        torch.cuda.synchronize()
+        out = {name: sum(e[k].elapsed_time(e[k + 1]) for e in evs) / reps for k, name in enumerate(self.STAGES)}
+        out["total"] = sum(e[0].elapsed_time(e[-1]) for e in evs) / reps
+        return out
+
+    def _mark(self, k):
+        if self._events is not None:
+            self._events[k].record()
+
     def _matvec_kernels(self, v, y, dot_out, pre):
         from gslm import _lib
         from gslm._lib import check, lib
         from gslm.params import raw_gaussians
+        self._mark(0)
         loc = self.local
         b = self._buffers()
         n, S, per, P = self.world_size, self.S, self.per, self.P
@@ -468,9 +502,11 @@ class GaussianShardedOperator:
                                          b["trec_send"].data_ptr() + 32 * c0 * S, S,
                                          None if opts is None else ctypes.byref(opts), loc.stream),
                   "gslm_tangent_views")
+        self._mark(1)
         # 2. every shard's records of my k-th view
         for k in range(per):
             self._all_to_all(b["trec_recv"][k], b["trec_send"][k])
+        self._mark(2)
         # 3. render my views from the exchanged tables: per-Gaussian screen-space sums
         for k, vr in enumerate(loc.views):
             opts = _lib.GslmMatvecOpts()
@@ -483,9 +519,11 @@ class GaussianShardedOperator:
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
                                           ctypes.byref(vs), ctypes.byref(opts), loc.stream), "gslm_matvec_view_ex")
             vr.tail_clean = True
+        self._mark(3)
         # 4. my shard's slices of every view's screen sums
         for k in range(per):
             self._all_to_all(b["screen_recv"][k], b["screen_send"][k])
+        self._mark(4)
         # 5. every view's chain over my shard, + D v, <v, y>
         fuse = dot_out is not None and self.hi > self.lo
         for c0 in range(0, nv, chunk):
@@ -505,4 +543,5 @@ class GaussianShardedOperator:
         e0, e1 = self.layout.offsets["exposure"]
         if e1 > e0:
             torch.mul(v[e0:e1], float(self._damps[6]), out=y[e0:e1])  # J has no exposure column
+        self._mark(5)
         return fuse

@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 4
+#define GSLM_ABI_VERSION 5
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -112,6 +112,11 @@ int gslm_preprocess(const gslm_view* view, const gslm_gaussians* g, void* geom, 
                     int32_t* out_radii, void* stream);
 /* Synchronous read of the number of (tile, Gaussian) pairs produced by gslm_preprocess. */
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out_num_rendered, void* stream);
+/* The same for n preprocessed geometries (geoms[k] over Ps[k] Gaussians) with ONE stream synchronisation:
+ * a batch of views (the line search's validation renders, gslm.lm.LossEvaluator) preprocesses every view first,
+ * then sizes every view's binning from one read-back instead of one round trip per view. */
+int gslm_num_rendered_many(const void* const* geoms, const int64_t* Ps, int32_t n, int64_t* out_num_rendered,
+                           void* stream);
 /* Binning + tile sort + ranges + per-tile blend.  out_color [3,H,W], out_invdepth [1,H,W] (nullable). */
 int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
                    int64_t num_rendered, void* image, size_t image_bytes, float* out_color,
@@ -215,6 +220,11 @@ typedef struct gslm_matvec_opts {
   const float* trec_in;
   /* gslm_gather_screen only: Gaussians between consecutive views' blocks of screen (0 means P). */
   int64_t screen_stride;
+  /* Device CG control block of gslm_cg_monitor, or NULL: when cg_ctl[0] != 0 (the solve's stopping tests have
+   * fired) the TANGENT, RENDER and GATHER kernels of this call return without work (and without writing y,
+   * the dot or the direction update), so a host can enqueue a whole CGLS schedule without reading the tests
+   * back each iteration. */
+  const double* cg_ctl;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
@@ -289,10 +299,21 @@ int gslm_xpby_dev(int64_t n, const float* s, const double* num_dev, const double
 int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                    float* x, float* s, void* scratch, double* gam_new_dev, void* stream);
 /* gslm_cg_update plus the residual monitor of conjugate_gradient.py:103-104 in the same pass:
- * *xg_dev = <x_new, g>, *xs_dev = <x_new, s_new> (g = J^T b).  scratch >= 3 * 1024 doubles. */
+ * *xg_dev = <x_new, g>, *xs_dev = <x_new, s_new> (g = J^T b).  scratch >= 3 * 1024 doubles.
+ * cg_ctl (or NULL): gslm_cg_monitor's control block; with cg_ctl[0] != 0 or *del_dev < 1e-20 (the early
+ * termination of conjugate_gradient.py:88-91) x and s are left untouched. */
 int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                            float* x, float* s, const float* g, void* scratch, size_t scratch_bytes,
-                           double* gam_new_dev, double* xg_dev, double* xs_dev, void* stream);
+                           double* gam_new_dev, double* xg_dev, double* xs_dev, const double* cg_ctl, void* stream);
+/* The stopping tests of cgls_damped (conjugate_gradient.py:88-117) on the device, one launch per inner iteration
+ * after gslm_cg_update_monitor (and after any cross-rank sums of its scalars).  cg_ctl = doubles
+ * [stop, iters, last_res, n_hist, history[max_hist]], initialised by the caller to [0, 0, +inf, 0, ...]:
+ *   *del < 1e-20 -> stop = 1;  res = (*b2 - *xg) - *xs is appended to history;  res > last_res -> stop = 2;
+ *   *gam_new < max(tol sqrt(*gam), atol) -> stop = 3;  otherwise iters += 1.
+ * Once stop != 0 every later gslm_cg_monitor / gslm_cg_update_monitor / product with opts->cg_ctl is a no-op. */
+int gslm_cg_monitor(const double* gam_dev, const double* gam_new_dev, const double* del_dev, const double* xg_dev,
+                    const double* xs_dev, const double* b2_dev, double tol, double atol, double* cg_ctl,
+                    int32_t max_hist, void* stream);
 /* *out_dev = sum of np per-block partials (second pass of the fused dots) */
 int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* stream);
 /* y += d[group] * x (the damping term D x) */
@@ -304,7 +325,9 @@ int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const 
  * 56-67, disable_ssim=True, and loss_scalar, solver/loss_image_state.py:16-19) ----
  * color / gt / residual / weight / seed are [3,H,W]; alpha_mask [H,W] or NULL (= 1).  Writes
  *   residual = m clamp(color, 0, 1) - gt          (NULL: not written)
- *   weight   = m^2 1[0 <= color <= 1]             (the per-pixel weight of gslm_matvec_view_ex)
+ *   weight   = m^2 1[0 <= color <= 1]             (the per-pixel weight of gslm_matvec_view_ex; NULL: not
+ *                                                  written -- with residual and seed NULL too, the loss alone:
+ *                                                  the line search's validation loss)
  *   seed     = -2 m 1[0 <= color <= 1] residual   (NULL: not written; gslm_backward's dL/dcolor for J^T b)
  * and *loss_dev (device double) = [*loss_dev if accumulate] + 2 sum residual^2 ([r; r] aliasing).
  * Deterministic (fixed two-pass reduction); scratch >= gslm_residual_scratch_bytes(H, W). */

@@ -26,7 +26,10 @@ DEFAULT_DAMP = {"xyz": 5e2, "features_dc": 5e-2, "features_rest": 5e-2, "scaling
 
 
 class OracleLMProblem:
-    def __init__(self, model, cams, bg, mask_xyz=True, damp=None, ssim=False, lambda_dssim=0.2):
+    def __init__(self, model, cams, bg, mask_xyz=True, damp=None, ssim=False, lambda_dssim=0.2, device="cpu",
+                 sh_projection=False):
+        # (device / sh_projection: the HIP LMProblem's keywords, accepted so gslm.lm.lm_step can build either;
+        # the oracle runs on the CPU in the reference's full layout)
         self.model, self.cams, self.bg = model, cams, bg
         self.mask_xyz = mask_xyz
         self.ssim, self.lambda_dssim = ssim, lambda_dssim
@@ -57,7 +60,9 @@ class OracleLMProblem:
 
     def evaluate(self):
         with torch.no_grad():
-            self.loss = sum(self._fac * (r.double() ** 2).sum() for r in self._residuals())
+            self.loss = torch.zeros((), dtype=torch.float64)
+            for r in self._residuals():
+                self.loss = self.loss + self._fac * (r.double() ** 2).sum()
         return self.loss
 
     def _flatten(self, tensors):
@@ -126,6 +131,26 @@ class OracleLMProblem:
 
     def zeros(self):
         return torch.zeros(self.layout.numel)
+
+
+class OracleLossEvaluator:
+    """The line search's validation loss on the oracle (gslm.lm.LossEvaluator's interface): 2 sum_b ||m_b
+    clamp01(R_b) - gt_b||^2 over `cams`, summed over the ranks by `reduce`."""
+
+    def __init__(self, model, cams, bg, device="cpu", batch=8, reduce=None):
+        self.prob = OracleLMProblem(model, cams, bg)
+        self.reduce = reduce
+
+    def evaluate(self):
+        loss = self.prob.evaluate().clone()
+        if self.reduce is not None:
+            self.reduce(loss)
+        return loss
+
+
+def cgls_solver(op, g, max_iter=10, restart_iter=10, check_every=True, verbose=False):
+    """cgls_ref in gslm.lm.lm_step's solver interface: (x, info)."""
+    return cgls_ref(op, g, max_iter, restart_iter), {"iters": None}
 
 
 def cgls_ref(op, g, max_iter, restart_iter, tol=1e-10, atol=0.0):

@@ -38,6 +38,17 @@ def main():
             "y_max": float((got["y"] - ref["y"]).abs().max() / ref["y"].abs().max()),
             "x_rel": float((got["x"] - ref["x"]).norm() / ref["x"].norm()),
         }
+    # the whole LM step (train_jvp.py:237-279) on the sharded path: Gaussian-sharded CG + all-reduced line search
+    import numpy as np
+    from gslm.lm import lm_step
+    from test_gpu_lm_step import _setup
+    d, L, m, cams, val = _setup()
+    r = lm_step(m, cams, val, torch.zeros(3), max_iter=10, restart_iter=10, exchange="gaussian")
+    s_ref = L["ten_s"].astype(np.float64)
+    out["lm_step"] = {
+        "ranks": r["ranks"], "best_alpha": r["best_alpha"], "best_alpha_ref": float(L["ten_best_alpha"]),
+        "step_rel": float(np.linalg.norm(r["step"].cpu().numpy() - s_ref) / np.linalg.norm(s_ref)),
+        "final_rel": abs(r["final_val_loss"] - float(L["ten_final_val_loss"])) / float(L["ten_final_val_loss"])}
     dist.barrier()
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)

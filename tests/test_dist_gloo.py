@@ -104,3 +104,75 @@ def test_shard_views_partition():
         parts = [shard_views(n, r, w) for r in range(w)]
         flat = [i for p in parts for i in p]
         assert flat == list(range(n))
+
+
+GROUPS = ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity", "exposure")
+
+
+def _golden_scene():
+    """The scene of tests/golden/lm_step_golden.npz (2 training views, 3 validation views, 400 Gaussians SH 1)."""
+    import numpy as np
+    from gslm.cameras import orbit_cameras
+    from gslm.model import GaussianModel
+    d = np.load(os.path.join(HERE, "golden", "solver_golden.npz"))
+    L = np.load(os.path.join(HERE, "golden", "lm_step_golden.npz"))
+    P, D, W, H, s0, nv = d["scene"]
+    D, W, H, nv = int(D), int(W), int(H), int(nv)
+    m = GaussianModel(D)
+    m.set_params(*(torch.from_numpy(d[f"in_{k}"]) for k in GROUPS))
+    m.active_sh_degree = D
+    cams = orbit_cameras(nv, W, H, seed=1, images=[torch.from_numpy(d[f"gt{i}"]) for i in range(nv)])
+    nval = sum(1 for k in L.files if k.startswith("val_gt"))
+    val = orbit_cameras(nval, W, H, seed=4, images=[torch.from_numpy(L[f"val_gt{i}"]) for i in range(nval)])
+    return L, m, cams, val
+
+
+def _lm_step_worker(rank, world, port, out_path, tag, sched):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from gslm.lm import lm_step
+    from oracle.lm_ref import OracleLMProblem, OracleLossEvaluator, cgls_solver
+    L, m, cams, val = _golden_scene()
+    out = lm_step(m, cams, val, torch.zeros(3), max_iter=sched[0], restart_iter=sched[1], device="cpu",
+                  backend=(OracleLMProblem, OracleLossEvaluator, cgls_solver))
+    params = [t.detach().clone() for t in m.params()]
+    torch.save({"out": {k: out[k] for k in ("start_loss", "final_val_loss", "best_alpha", "trace", "ranks")},
+                "step": out["step"], "params": params}, out_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tag,sched", [("ref", (2, 1)), ("ten", (10, 10))])
+def test_sharded_lm_step_matches_reference_golden(tmp_path, tag, sched):
+    """gslm.lm.lm_step across 2 ranks (train_jvp.py:237-279, SURVEY 8(e) 'Line search. Sharded the same way'): one
+    training view per rank with Gaussian-sharded CG vectors, the 3 validation views split 2 + 1 with one all-reduced
+    loss per line-search point, the step gathered whole and applied on both ranks.  Both ranks must end with
+    bitwise identical parameters, and the step, best_alpha, search trace, final loss and parameters must match
+    the reference's (lm_step_golden.npz) at the single-process GPU test's tolerances.  The per-rank problem is the
+    oracle restatement; the driver, sharding and reductions are the product's."""
+    import numpy as np
+    out = str(tmp_path / "r")
+    mp.start_processes(_lm_step_worker, args=(2, _free_port(), out, tag, sched), nprocs=2, start_method="spawn",
+                       join=True)
+    r0, r1 = (torch.load(out + f".{r}", weights_only=True) for r in (0, 1))
+    for a, b in zip(r0["params"], r1["params"]):
+        assert torch.equal(a, b)
+    assert torch.equal(r0["step"], r1["step"])
+    L = np.load(os.path.join(HERE, "golden", "lm_step_golden.npz"))
+    o = r0["out"]
+    assert o["ranks"] == 2
+    assert abs(o["start_loss"] - float(L[f"{tag}_start_loss"])) <= 1e-5 * float(L[f"{tag}_start_loss"])
+    s_ref = L[f"{tag}_s"].astype(np.float64)
+    s = r0["step"].numpy().astype(np.float64)
+    assert np.linalg.norm(s - s_ref) <= 1e-4 * np.linalg.norm(s_ref)
+    assert o["best_alpha"] == float(L[f"{tag}_best_alpha"])
+    assert [a for a, _ in o["trace"]] == list(L[f"{tag}_trace_alpha"])
+    ref = L[f"{tag}_trace_loss"]
+    assert np.abs(np.array([v for _, v in o["trace"]]) - ref).max() <= 1e-4 * ref.max()
+    assert abs(o["final_val_loss"] - float(L[f"{tag}_final_val_loss"])) <= 1e-4 * float(L[f"{tag}_final_val_loss"])
+    scale = float(L[f"{tag}_best_alpha"]) * np.abs(s_ref).max()
+    for k, t in zip(GROUPS, r0["params"]):
+        err = np.abs(t.numpy().astype(np.float64) - L[f"{tag}_out_{k}"]).max()
+        assert err <= 1e-4 * scale + 1e-6, (k, err, scale)
