@@ -382,8 +382,9 @@ def main():
         cc = orbit_cameras(1, W, H, seed=1)[0]
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
         r = cpu_matvec_rate(cm, cc, torch.zeros(3), n_tiles=args.cpu_tiles, repeats=3, threads=threads)
-        from oracle.cpu_baseline import cpu_config0_times, host_info
+        from oracle.cpu_baseline import cpu_config0_times, cpu_config1_forward, host_info
         c0 = cpu_config0_times(repeats=5, threads=threads)
+        c1 = cpu_config1_forward(repeats=5, threads=threads, W=W, H=H, s0=args.s0)
         cpu = {"value": 1.0 / r["matvec_s"], "unit": "view-matvec/s", "cores": r["threads"], "kind": "port",
                "sample": (f"oracle/torch_raster.py (PyTorch CPU, {r['threads']} threads, {r['cpu_model']}): "
                           f"all {args.P} Gaussians through preprocess+binning with forward-AD and autograd "
@@ -392,8 +393,11 @@ def main():
                           f"their own) scaled by {r['ntiles']}/{r['n_tiles']}; each phase the median of 3"),
                "raster_mpix_s": W * H / r["forward_s"] / 1e6,
                "host": host_info(),
-               "threads_note": "OMP_NUM_THREADS threads (the GPU box's CPU share for this job; os.cpu_count() "
-                               "reports the whole machine)",
+               "threads_note": "OMP_NUM_THREADS threads: the CPU share the GPU box gives one GPU's job (16 of the "
+                               "host's threads; os.cpu_count() counts the whole 8-GPU host, whose other threads "
+                               "belong to the other GPUs' jobs, so timing on all of them would not be this "
+                               "job's baseline)",
+               "configs1_forward": c1,
                "configs0": dict(c0, config="BASELINE configs[0]: 2000 Gaussians SH0, one 256x256 view, oracle "
                                            "forward / JVP / VJP, 1 warm-up + median of 5, no extrapolation")}
 

@@ -137,7 +137,10 @@ static int make_gauss(const gslm_gaussians* in, const ViewK* v, GaussK* g, bool 
   return GSLM_OK;
 }
 
-int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* radii, hipStream_t s) {
+// order_mode (gslm_preprocess_ordered): 0 sort, 1 sort and copy the order out to depth_order, 2 take the order from
+// depth_order instead of sorting
+int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* radii, hipStream_t s,
+                  uint32_t* depth_order = nullptr, int order_mode = 0) {
   int st = launch_preprocess(v, g, gb, radii, s);
   if (st) return st;
   const int64_t P = g.P;
@@ -145,11 +148,17 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
     GSLM_HIP_CHECK(hipMemsetAsync(gb.counters, 0, 4, s));
     return GSLM_OK;
   }
-  // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass)
-  bool alt = false;
-  st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true);
-  if (st) return st;
-  if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  if (order_mode == 2) {
+    GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  } else {
+    // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass)
+    bool alt = false;
+    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true);
+    if (st) return st;
+    if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+    if (order_mode == 1)
+      GSLM_HIP_CHECK(hipMemcpyAsync(depth_order, gb.sorted_idx, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  }
   // tile-count scans in index order (gradient-row offsets goff) and in depth order (duplicate offsets)
   return exclusive_scan_u32_dual(gb.tiles, gb.sorted_idx, gb.goff, gb.offsets, P, gb.scan_tmp, gb.counters + 1,
                                  gb.counters, s);
@@ -183,6 +192,21 @@ int gslm_preprocess(const gslm_view* view, const gslm_gaussians* gi, void* geom,
   GeomBufs gb;
   geom_layout(g.P, geom, &gb);
   return do_preprocess(v, g, gb, out_radii, (hipStream_t)stream);
+}
+
+int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes,
+                            int32_t* out_radii, uint32_t* depth_order, int32_t order_mode, void* stream) {
+  if (order_mode < 0 || order_mode > 2) { set_error("preprocess_ordered: order_mode must be 0, 1 or 2"); return GSLM_ERR_INVALID; }
+  if (order_mode && gi && gi->P > 0 && !depth_order) { set_error("preprocess_ordered: NULL depth_order"); return GSLM_ERR_INVALID; }
+  ViewK v;
+  GaussK g;
+  int st = make_view(view, gi ? gi->max_coeffs : 0, &v);
+  if (st) return st;
+  if ((st = make_gauss(gi, &v, &g, false))) return st;
+  if (geom_bytes < gslm_geom_bytes(g.P) || (!geom && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
+  GeomBufs gb;
+  geom_layout(g.P, geom, &gb);
+  return do_preprocess(v, g, gb, out_radii, (hipStream_t)stream, depth_order, order_mode);
 }
 
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {

@@ -41,7 +41,14 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   depth_key[i] = 0xFFFFFFFFu;
   if (radii_out) radii_out[i] = 0;
   PreOut o;
-  if (!preprocess_one<RAW>(v, g, i, o)) return;
+  o.depth = 0.f;
+  const bool vis = preprocess_one<RAW>(v, g, i, o);
+  // Every Gaussian in front of the near plane gets its depth key, culled by its footprint or not: the depth order
+  // then depends on means3D and the view alone, so one view's order is reusable while xyz is unchanged (the LM
+  // step freezes xyz, train_jvp.py:221-227: gslm_preprocess_ordered).  The point list is the same either way
+  // (Gaussians culled later emit no tile).
+  if (o.depth > 0.2f) depth_key[i] = __float_as_uint(o.depth);
+  if (!vis) return;
 
   const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
   const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
@@ -49,7 +56,6 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   rec[RECS * i + 0] = r0;
   rec[RECS * i + 1] = r1;
   rec[RECS * i + 2] = r2;
-  depth_key[i] = __float_as_uint(o.depth);
   tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
   rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
   clampw[i] = o.clamped;  // read only where tiles[i] != 0

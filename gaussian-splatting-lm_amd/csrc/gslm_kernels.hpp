@@ -247,6 +247,7 @@ template <bool RAW>
 __device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, int64_t i, PreOut& o) {
   const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
   const float tz = tp_row(v.view, x, y, z, 2);
+  o.depth = tz;  // set before any cull: the depth order of every Gaussian in front of the near plane
   if (!(tz > 0.2f)) return false;
   const float tx = tp_row(v.view, x, y, z, 0), ty = tp_row(v.view, x, y, z, 1);
   const float hx = tp_row(v.proj, x, y, z, 0), hy = tp_row(v.proj, x, y, z, 1), hw = tp_row(v.proj, x, y, z, 3);

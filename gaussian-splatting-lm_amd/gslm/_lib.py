@@ -86,6 +86,9 @@ EXPORTS = {
                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_num_rendered": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
                                          ctypes.c_void_p]),
+    "gslm_preprocess_ordered": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
+                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_int32, ctypes.c_void_p]),
     "gslm_num_rendered_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,

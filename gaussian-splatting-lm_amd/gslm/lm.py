@@ -407,7 +407,7 @@ class LMProblem:
             arr[k] = vw
         return arr
 
-    def screen_products(self, v, screen, pre=None):
+    def screen_products(self, v, screen, pre=None, cg_ctl=None):
         """screen[b] = this rank's view b's per-Gaussian screen-space sums S_b^T W_b J_b v (P x 8,
         GSLM_STAGE_SCREEN); pre as in matvec_dot (applied with the first view)."""
         g = raw_gaussians(self.model)
@@ -421,6 +421,7 @@ class LMProblem:
             opts.stages = 1 | 2 | 16  # TANGENT | RENDER | SCREEN
             opts.flags = MV_TAIL_CLEAN if vr.tail_clean else 0
             opts.screen_out = screen[b].data_ptr()
+            opts.cg_ctl = cg_ctl
             if pre is not None and b == 0:
                 ss = self._pre_opts(opts, v, pre)  # noqa: F841
             check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
@@ -744,7 +745,9 @@ class LossEvaluator:
     with disable_ssim=True over the validation views: 2 sum_b ||m_b clamp01(R_b) - gt_b||^2) on the HIP forward.
 
     Per view: gslm_preprocess -> gslm_rasterize -> gslm_lm_residual in its loss-only form (no residual, weight or
-    seed images).  Views run in batches of `batch` workspaces: a batch's preprocesses are enqueued first and one
+    seed images).  The depth order of each view depends on xyz alone, which the LM step freezes
+    (train_jvp.py:221-227): it is sorted at the first evaluation and reused by later ones while model._xyz is the
+    same tensor at the same version (gslm_preprocess_ordered; the same point list, bitwise).  Views run in batches of `batch` workspaces: a batch's preprocesses are enqueued first and one
     gslm_num_rendered_many read-back sizes all their binnings (one host round trip per batch, not per view); the
     loss accumulates in a device double, in view order.  `reduce`: a callable summing the device double over the
     ranks that hold the other views (the multi-GPU line search, gslm.parallel.allreduce_loss)."""
@@ -769,6 +772,7 @@ class LossEvaluator:
         self.res_scratch = torch.empty(lib.gslm_residual_scratch_bytes(1, 1) // 8, dtype=torch.float64,
                                        device=device)
         self.num_rendered = [0] * len(cams)
+        self._order_key, self._orders = None, [None] * len(cams)
 
     def _slot(self, k, P, H, W):
         sl = self.slots[k]
@@ -785,12 +789,20 @@ class LossEvaluator:
         P = g.P
         loss = torch.zeros((), dtype=torch.float64, device=self.device)
         V = len(self.views)
+        xyz = self.model._xyz
+        key = (xyz.data_ptr(), xyz._version, P)
+        if key != self._order_key:  # xyz moved: sort again
+            self._order_key, self._orders = key, [None] * V
         for b0 in range(0, V, self.batch):
             idx = list(range(b0, min(V, b0 + self.batch)))
             slots = [self._slot(k, P, self.views[i].image_height, self.views[i].image_width) for k, i in enumerate(idx)]
             for sl, i in zip(slots, idx):
-                check(lib.gslm_preprocess(ctypes.byref(self.views[i]), ctypes.byref(g), sl["geom"].data_ptr(),
-                                          sl["geom"].numel(), None, self.stream), "gslm_preprocess")
+                mode = 2 if self._orders[i] is not None else 1
+                if mode == 1:
+                    self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(g), sl["geom"].data_ptr(),
+                                                  sl["geom"].numel(), None, self._orders[i].data_ptr(), mode,
+                                                  self.stream), "gslm_preprocess_ordered")
             geoms = (ctypes.c_void_p * len(idx))(*[sl["geom"].data_ptr() for sl in slots])
             Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
             Ns = (ctypes.c_int64 * len(idx))()
@@ -815,11 +827,14 @@ class LossEvaluator:
         return loss
 
 
-def update_params(model, layout, step, scale):
-    """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step."""
+def update_params(model, layout, step, scale, skip_xyz=False):
+    """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step.  skip_xyz: the step's xyz
+    group is zero by construction (the LM step's param mask, train_jvp.py:221-227), so adding it would change no
+    value -- it is left alone, which keeps model._xyz's version (the line search's cached depth orders)."""
     v = layout.views(step)
     with torch.no_grad():
-        model._xyz.add_(v["xyz"], alpha=scale)
+        if not skip_xyz:
+            model._xyz.add_(v["xyz"], alpha=scale)
         model._features_dc.add_(v["features_dc"], alpha=scale)
         model._features_rest.add_(v["features_rest"], alpha=scale)
         model._scaling.add_(v["scaling"], alpha=scale)
@@ -894,16 +909,16 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     alpha = 2.0
     best_alpha, best_loss = alpha, math.inf
     trace = []
-    update_params(model, full, s, alpha)
+    update_params(model, full, s, alpha, skip_xyz=mask_xyz)
     for _ in range(6):
         vl = float(val.evaluate())
         trace.append((alpha, vl))
         if vl < best_loss:
             best_loss, best_alpha = vl, alpha
         new_alpha = alpha * 0.5
-        update_params(model, full, s, new_alpha - alpha)
+        update_params(model, full, s, new_alpha - alpha, skip_xyz=mask_xyz)
         alpha = new_alpha
-    update_params(model, full, s, best_alpha - alpha)
+    update_params(model, full, s, best_alpha - alpha, skip_xyz=mask_xyz)
     final = float(val.evaluate())
     lap("line_search_ms")
     out = dict(start_loss=start_loss, final_val_loss=final, best_alpha=best_alpha, cg=info, step=s, trace=trace,

@@ -84,6 +84,7 @@ def _staged(fn, *tensors):
 class ShardedOperator:
     SCREEN_FLOATS = 8  # per (view, Gaussian) in the screen exchange
     supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
+    supports_cg_ctl = True  # cgls_fused's device control block, passed to the local products
 
     def __init__(self, local, group=None, all_cams=None, exchange="auto"):
         self.local = local
@@ -132,19 +133,21 @@ class ShardedOperator:
         self.local.rhs(out)
         return self._allreduce(out)
 
-    def matvec_dot(self, v, y, dot_out, pre=None):
+    def matvec_dot(self, v, y, dot_out, pre=None, cg_ctl=None):
         kw = {} if pre is None else {"pre": pre}
+        if cg_ctl is not None:
+            kw["cg_ctl"] = cg_ctl
         if not collectives_on(self.world_size):
             return self.local.matvec_dot(v, y, dot_out, **kw)
         if self.exchange == "screen":
-            return self._matvec_screen(v, y, dot_out, pre)
+            return self._matvec_screen(v, y, dot_out, pre, cg_ctl)
         # every rank holds the same s, p and scalars, so the deferred p update stays rank-local
         self.local.local_normal_matvec(v, y, damp=False, **kw)
         self._allreduce(y)
         self.local.damp_add(v, y)
         return False
 
-    def _matvec_screen(self, v, y, dot_out, pre):
+    def _matvec_screen(self, v, y, dot_out, pre, cg_ctl=None):
         per = (len(self.all_cams) + self.world_size - 1) // self.world_size
         P = self.local.layout.P
         if self._screen is None:
@@ -153,13 +156,13 @@ class ShardedOperator:
             self._screen_all = torch.empty(self.world_size * per, P, self.SCREEN_FLOATS, dtype=torch.float32,
                                            device=dev)
             self._views_all = self.local.views_for(self.all_cams, pad_to=self.world_size * per)
-        self.local.screen_products(v, self._screen, pre=pre)
+        self.local.screen_products(v, self._screen, pre=pre, cg_ctl=cg_ctl)
         _all_gather_into(self._screen_all, self._screen, self.group)
         self.local.gather_screen(self._views_all, self._screen_all, v, y, dot_out)
         return dot_out is not None
 
-    def matvec(self, v, y):
-        self.matvec_dot(v, y, None)
+    def matvec(self, v, y, cg_ctl=None):
+        self.matvec_dot(v, y, None, cg_ctl=cg_ctl)
         return y
 
 
@@ -231,6 +234,7 @@ class GaussianShardedOperator:
 
     exchange = "gaussian"
     supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
+    supports_cg_ctl = True  # cgls_fused's device control block: the tile pass of a stopped solve returns at once
 
     def __init__(self, local, group=None, all_cams=None):
         self.local = local
@@ -391,11 +395,11 @@ class GaussianShardedOperator:
             dy[name].add_(dv[name], alpha=d)
         return y
 
-    def matvec(self, v, y):
-        self.matvec_dot(v, y, None)
+    def matvec(self, v, y, cg_ctl=None):
+        self.matvec_dot(v, y, None, cg_ctl=cg_ctl)
         return y
 
-    def matvec_dot(self, v, y, dot_out, pre=None):
+    def matvec_dot(self, v, y, dot_out, pre=None, cg_ctl=None):
         if not self.kernel_path:
             if pre is not None:
                 raise ValueError("the fused direction update needs the HIP operator")
@@ -405,7 +409,7 @@ class GaussianShardedOperator:
             self.shard(yf, y)
             self.damp_add_shard(v, y)
             return False
-        return self._matvec_kernels(v, y, dot_out, pre)
+        return self._matvec_kernels(v, y, dot_out, pre, cg_ctl)
 
     # ------------------------------------------------------------------ HIP path
     def _buffers(self):
@@ -469,7 +473,7 @@ class GaussianShardedOperator:
         if self._events is not None:
             self._events[k].record()
 
-    def _matvec_kernels(self, v, y, dot_out, pre):
+    def _matvec_kernels(self, v, y, dot_out, pre, cg_ctl=None):
         from gslm import _lib
         from gslm._lib import check, lib
         from gslm.params import raw_gaussians
@@ -514,6 +518,7 @@ class GaussianShardedOperator:
             opts.flags = 1 if vr.tail_clean else 0  # GSLM_MV_TAIL_CLEAN
             opts.screen_out = b["screen_send"][k].data_ptr()
             opts.trec_in = b["trec_recv"][k].data_ptr()
+            opts.cg_ctl = cg_ctl
             check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
                                           loc.weights[k].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),

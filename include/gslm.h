@@ -110,6 +110,15 @@ size_t gslm_scratch_bytes(int64_t P, int64_t num_rendered); /* backward / jvp / 
 /* Per-Gaussian preprocess, depth sort and tile-count scan.  Writes radii (int32 [P]) if non-NULL. */
 int gslm_preprocess(const gslm_view* view, const gslm_gaussians* g, void* geom, size_t geom_bytes,
                     int32_t* out_radii, void* stream);
+/* gslm_preprocess with a reusable depth order.  The depth order (the stable sort of every Gaussian in front of the
+ * near plane by view-space depth, index order on ties; Gaussians culled later by their footprint emit no tile, so
+ * the point list is the same whatever their place) depends on means3D and the view alone.
+ *   order_mode 0: as gslm_preprocess;  1: also copy the order to depth_order[P];
+ *   2: take the order from depth_order[P] -- written by a mode-1 call on the same view with the same means3D --
+ *      instead of sorting (the LM line search renders each validation view at 7 step sizes with xyz frozen,
+ *      train_jvp.py:221-227,262-279: the same point list, bitwise, without the four depth-sort passes). */
+int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* g, void* geom, size_t geom_bytes,
+                            int32_t* out_radii, uint32_t* depth_order, int32_t order_mode, void* stream);
 /* Synchronous read of the number of (tile, Gaussian) pairs produced by gslm_preprocess. */
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out_num_rendered, void* stream);
 /* The same for n preprocessed geometries (geoms[k] over Ps[k] Gaussians) with ONE stream synchronisation:

@@ -183,3 +183,35 @@ def host_info():
         affinity = None
     return {"os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": _cpu_model(),
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_config1_forward(repeats=5, threads=None, P=100_000, W=1920, H=1080, s0=0.005):
+    """BASELINE.json configs[1]'s forward on the host cores, timed whole (SURVEY 8(d) "CPU baseline": config 2's
+    forward on the CPU when it finishes in minutes): P = 100k synthetic Gaussians, SH 3, one 1080p view through the
+    full oracle rasterizer (preprocess, binning, every tile's blend), no sampling or extrapolation; 1 warm-up then
+    the median of `repeats`.  Returns seconds per forward, Mpix/s and the thread count."""
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    if threads:
+        torch.set_num_threads(threads)
+    model = synthetic_gaussians(P, 3, seed=0, s0=s0)
+    cam = orbit_cameras(1, W, H, seed=1)[0]
+    st = tr.settings_from_camera(cam, torch.zeros(3), 3)
+    with torch.no_grad():
+        a = dict(means3D=model.get_xyz, opacities=model.get_opacity, scales=model.get_scaling,
+                 rotations=model.get_rotation, shs=model.get_features)
+
+        def fwd():
+            tr.rasterize(a["means3D"], torch.zeros_like(a["means3D"]), a["opacities"], st, shs=a["shs"],
+                         scales=a["scales"], rotations=a["rotations"])
+
+        fwd()
+        ts = []
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            fwd()
+            ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    return {"forward_s": t, "mpix_s": W * H / t / 1e6, "threads": torch.get_num_threads(), "repeats": repeats,
+            "config": f"BASELINE configs[1] forward: {P} Gaussians SH3, one {W}x{H} view, oracle rasterizer timed "
+                      "whole (1 warm-up + median)"}

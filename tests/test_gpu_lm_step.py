@@ -157,4 +157,13 @@ def test_loss_evaluator_equals_lmproblem_evaluate():
     for batch in (1, 2, 8):
         ev = LossEvaluator(m, cams, torch.zeros(3), batch=batch)
         assert float(ev.evaluate()) == ref
-        assert float(ev.evaluate()) == ref  # reused workspaces
+        assert float(ev.evaluate()) == ref  # reused workspaces and the cached depth orders (gslm_preprocess_ordered)
+    # a line-search-like step on everything but xyz: the cached orders stay valid (same point lists, bitwise)
+    with torch.no_grad():
+        m._opacity.add_(0.7 * torch.randn(m._opacity.shape, generator=torch.Generator().manual_seed(5)).cuda())
+        m._scaling.add_(0.3 * torch.randn(m._scaling.shape, generator=torch.Generator().manual_seed(6)).cuda())
+    assert float(ev.evaluate()) == float(LMProblem(m, cams, torch.zeros(3)).evaluate())
+    # xyz moves: the evaluator notices (tensor version) and sorts again
+    with torch.no_grad():
+        m._xyz.add_(0.05 * torch.randn(m._xyz.shape, generator=torch.Generator().manual_seed(7)).cuda())
+    assert float(ev.evaluate()) == float(LMProblem(m, cams, torch.zeros(3)).evaluate())
