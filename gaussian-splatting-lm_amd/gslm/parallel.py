@@ -236,10 +236,14 @@ class GaussianShardedOperator:
     supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
     supports_cg_ctl = True  # cgls_fused's device control block: the tile pass of a stopped solve returns at once
 
-    def __init__(self, local, group=None, all_cams=None):
+    def __init__(self, local, group=None, all_cams=None, emulate=None):
+        """emulate=(rank, n): timing only -- run rank `rank` of an n-rank job's per-rank kernels in one process, each
+        collective replaced by a local copy of the same shape (the products are NOT the n-rank job's; the kernels'
+        sizes and control flow are: tile-pass decisions are frozen at the primal, independent of tangent values)."""
         self.local = local
         self.group = group
-        self.rank, self.world_size = world()
+        self._emulate = emulate is not None
+        self.rank, self.world_size = emulate if self._emulate else world()
         self._slot_index = {}  # allreduce_scalars' device index tensors, per slot tuple
         full = local.layout
         if getattr(full, "rest_projected", False):
@@ -274,12 +278,12 @@ class GaussianShardedOperator:
 
     # ------------------------------------------------------------------ collectives
     def _allreduce(self, t):
-        if collectives_on(self.world_size):
+        if collectives_on(self.world_size) and not self._emulate:
             _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
         return t
 
     def _all_to_all(self, out, inp):
-        if not collectives_on(self.world_size):
+        if not collectives_on(self.world_size) or self._emulate:
             out.copy_(inp)
             return
         _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
@@ -288,7 +292,7 @@ class GaussianShardedOperator:
         """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks.  One slot (the CG
         loop's delta and gamma' without the residual monitor): in place on the 8-byte view, no gather / scatter
         kernels and no host-to-device index copy around the collective."""
-        if not collectives_on(self.world_size):
+        if not collectives_on(self.world_size) or self._emulate:
             return
         slots = tuple(slots)
         if len(slots) == 1:
@@ -332,7 +336,9 @@ class GaussianShardedOperator:
             pack[:self.hi - self.lo, c:c + w] = rows[name]
             c += w
         allp = torch.empty(n * S, F, dtype=vec.dtype, device=vec.device)
-        if collectives_on(n):
+        if self._emulate:
+            allp.copy_(pack.repeat(n, 1))
+        elif collectives_on(n):
             _all_gather_into(allp, pack, self.group)
         else:
             allp.copy_(pack)
@@ -346,7 +352,7 @@ class GaussianShardedOperator:
         if self.layout.n_exposure:
             a0, a1 = self.layout.offsets["exposure"]
             out[e0:e1] = vec[a0:a1]
-        if collectives_on(n):
+        if collectives_on(n) and not self._emulate:
             ex = out[e0:e1].clone()
             self._allreduce(ex)
             out[e0:e1] = ex
