@@ -264,6 +264,29 @@ int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, 
   return launch_render_fwd(v, gb, bb, ib, out_color, out_invdepth, s);
 }
 
+size_t gslm_loss_scratch_bytes(int32_t H, int32_t W) {
+  const int64_t ntiles = (int64_t)((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y);
+  return (size_t)(ntiles > 0 ? ntiles : 1) * sizeof(double);
+}
+
+int gslm_rasterize_loss(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes, int64_t N,
+                        const float* gt, const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
+                        int32_t accumulate, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (binning_bytes < gslm_binning_bytes(N, v.H, v.W)) { set_error("binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (scratch_bytes < gslm_loss_scratch_bytes(v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
+  if (!gt || !loss_dev || !scratch) { set_error("rasterize_loss: NULL gt / loss / scratch"); return GSLM_ERR_INVALID; }
+  GeomBufs gb;
+  BinBufs bb;
+  geom_layout(P, geom, &gb);
+  bin_layout(N, v.gx * v.gy, binning, &bb);
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = launch_binning(v, P, gb, bb, N, s))) return st;
+  return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0, s);
+}
+
 int gslm_forward(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, void* binning,
                  size_t binning_bytes, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
                  int32_t* out_radii, int64_t* out_num_rendered, void* stream) {

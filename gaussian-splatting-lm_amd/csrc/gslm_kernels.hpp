@@ -65,16 +65,9 @@ struct PreOut {
 // Exact math: alpha >= 1/255  <=>  Q(d) = A dx^2 + C dy^2 + 2 B dx dy <= t = 2 ln(255 o), with
 // (A, B, C) the stored conic.  The float evaluation of Q in the tile passes (-ffp-contract=off, a
 // handful of roundings per term, |2 B dx dy| <= max(A, C) |d|^2) errs by at most 14 eps (A + C) |d|^2,
-// so every pixel a pass can accept satisfies d^T (Q - e I) d <= t with e = 32 eps (A + C).  The
-// quadrant test bounds min over the quadrant of d^T (Q - e I) d from below and rejects the quadrant only
-// when that bound exceeds tq = t * 1.02 + 1e-4 (exp / log / 1/255-constant rounding), rounded up to float.
-//
-// The minimisation runs in float (k_duplicate evaluates it for every (tile, Gaussian) pair: in double it
-// cost 46 of the kernel's 80 us at 1M Gaussians / 1080p).  Its value at the chosen point is lowered by a
-// rounding bound before the comparison: 2e-6 of the terms' magnitude (a few float roundings of a
-// 5-term expression, 8x over), the gradient times the rounding of the pixel offsets (tile origin minus
-// centre: <= 4e-7 (|gx| + |gy| + 8192)), and 1e-5 absolute (the edge minimiser's rounding is second
-// order).  Looser than exact only ever keeps a quadrant, so the cull stays exact.
+// so every pixel a pass can accept satisfies d^T (Q - e I) d <= tq with e = 32 eps (A + C) and
+// tq = t * 1.02 + 1e-4 (exp / log / 1/255-constant rounding), rounded up to float.  The quadrant test keeps a
+// quadrant whenever that ellipse can reach it (quad_mask below), evaluated in float with widened bounds.
 
 // tq for effective opacity o; negative when o <= 1/255 (no pixel can ever pass).
 __device__ __forceinline__ float alpha_threshold(float op_eff) {
@@ -87,8 +80,18 @@ __device__ __forceinline__ float alpha_threshold(float op_eff) {
 
 // Per-Gaussian part of the quadrant test (k_duplicate prepares it once and tests every tile of the
 // rect).  mode: 0 = reaches no pixel, 1 = treat every quadrant as reachable, 2 = test.
+//
+// The test works on E' = {d : a x^2 + 2 b x y + c y^2 <= t} with (a, b, c) = the conic minus e I (e above) and t = tq:
+// every pixel a tile pass can accept lies in E'.  For a band of pixel rows y in [ya, yb] (offsets from the centre)
+// E' spans x in [xmin(band), xmax(band)]: x_hi(y) = (-b y + sqrt(t a - det y^2)) / a is concave, so its maximum over
+// the band is at the band point nearest y_r = -b x_r / c (the ellipse's rightmost point, x_r = sqrt(t c / det)),
+// and by symmetry the minimum of x_lo(y) is at the point nearest -y_r.  A quadrant is kept when its columns meet
+// that interval -- two square roots per band of 8 rows, for both quadrants of the band (the round-2 test bounded
+// min over each quadrant of the form from its facing edges: four rectangles per entry, ~4x the VALU).  The
+// interval is widened by 1e-4 of its terms' magnitude + 0.01 px, far above the few float roundings of its
+// evaluation: looser only ever keeps a quadrant, so the cull stays exact.
 struct QuadCull {
-  float gx, gy, a, b, c, nba, nbc, tq, dpos;
+  float gx, gy, ia, b, det, ta, ydom, yr, sqm;
   int mode;
 };
 
@@ -105,50 +108,40 @@ __device__ __forceinline__ QuadCull quad_cull_prep(float gx, float gy, float A, 
     return q;
   }
   const float e = 32.0f * 5.9604644775390625e-8f * (A + C);
-  q.a = A - e;
-  q.c = C - e;
-  q.b = B;
-  // unbounded, nearly degenerate (the float minimiser would be ill-conditioned) or NaN: every quadrant
-  if (!(q.a > 0.0f && q.c > 0.0f && q.a * q.c - q.b * q.b > 1e-6f * (q.a * q.c))) {
+  const float a = A - e, c = C - e;
+  const float det = a * c - B * B;
+  // unbounded, nearly degenerate (ill-conditioned), an infinite threshold (the exhaustive traversal) or NaN:
+  // every quadrant
+  if (!(a > 0.0f && c > 0.0f && det > 1e-6f * (a * c) && tq < INFINITY)) {
     q.mode = 1;
     return q;
   }
-  q.nba = -q.b / q.a;  // edge minimisers; their rounding changes the edge minimum only to second order
-  q.nbc = -q.b / q.c;
   q.gx = gx;
   q.gy = gy;
-  q.tq = tq;
-  q.dpos = 4e-7f * (fabsf(gx) + fabsf(gy) + 8192.0f);
+  q.ia = 1.0f / a;
+  q.b = B;
+  q.det = det;
+  q.ta = tq * a;
+  q.ydom = sqrtf(q.ta / det) * 1.0001f + 0.01f;  // |y| over E'
+  q.yr = -B * sqrtf(tq * c / det) / c;          // y of E''s rightmost point
+  // sqrt(t a - det y^2) near the band ends of E' loses up to sqrt(eps t a) to the cancellation: widen by
+  // sqrt(1e-6 t a) / a (16x that), besides the relative 1e-4 and the 0.01 px of band_x_extent
+  q.sqm = sqrtf(1e-6f * q.ta) * q.ia;
   return q;
 }
 
-// Q at the offset (x, y) minus its rounding bound (see above).
-__device__ __forceinline__ float q_lower(const QuadCull& q, float x, float y) {
-  const float ax = q.a * x, by = q.b * y, bx = q.b * x, cy = q.c * y;
-  const float val = (ax + 2.0f * by) * x + cy * y;
-  const float mag = (fabsf(ax) + 2.0f * fabsf(by)) * fabsf(x) + fabsf(cy * y);
-  const float grad = 2.0f * (fabsf(ax) + fabsf(by) + fabsf(bx) + fabsf(cy));
-  return val - (2e-6f * mag + grad * q.dpos + 1e-5f);
-}
-
-// Lower bound of min over the rectangle [x0, x1] x [y0, y1] (offsets from the centre) of
-// a x^2 + 2 b x y + c y^2 (positive definite): 0 if the rectangle holds the centre, else the minimum is on an
-// edge that FACES the centre (the segment from any point of the rectangle to the centre, along which the form
-// decreases, leaves the rectangle through such an edge), so at most one vertical and one horizontal edge are
-// evaluated.
-__device__ __forceinline__ float rect_qmin(const QuadCull& q, float x0, float x1, float y0, float y1) {
-  const bool in_x = x0 <= 0.0f && x1 >= 0.0f, in_y = y0 <= 0.0f && y1 >= 0.0f;
-  if (in_x && in_y) return 0.0f;
-  float best = INFINITY;
-  if (!in_x) {  // the vertical edge nearer the centre
-    const float xe = x0 > 0.0f ? x0 : x1;
-    best = q_lower(q, xe, fminf(fmaxf(q.nbc * xe, y0), y1));
-  }
-  if (!in_y) {  // the horizontal edge nearer the centre
-    const float ye = y0 > 0.0f ? y0 : y1;
-    best = fminf(best, q_lower(q, fminf(fmaxf(q.nba * ye, x0), x1), ye));
-  }
-  return best;
+// [lo, hi] = the x extent of E' over the row band [ya, yb] (offsets), widened; false when the band misses E'.
+__device__ __forceinline__ bool band_x_extent(const QuadCull& q, float ya, float yb, float& lo, float& hi) {
+  const float y0 = fmaxf(ya, -q.ydom), y1 = fminf(yb, q.ydom);
+  if (!(y0 <= y1)) return false;
+  const float yh = fminf(fmaxf(q.yr, y0), y1), yl = fminf(fmaxf(-q.yr, y0), y1);
+  const float sh = sqrtf(fmaxf(q.ta - q.det * yh * yh, 0.0f)), sl = sqrtf(fmaxf(q.ta - q.det * yl * yl, 0.0f));
+  const float bh = q.b * yh, bl = q.b * yl;
+  hi = (sh - bh) * q.ia;
+  lo = -(sl + bl) * q.ia;
+  hi += 1e-4f * (fabsf(bh) + sh) * q.ia + q.sqm + 0.01f;
+  lo -= 1e-4f * (fabsf(bl) + sl) * q.ia + q.sqm + 0.01f;
+  return true;
 }
 
 // Quadrant mask of a Gaussian in tile (tile_x, tile_y): bit s set when its alpha region can reach
@@ -158,9 +151,15 @@ __device__ __forceinline__ uint32_t quad_mask(const QuadCull& q, int tile_x, int
   const float bx = (float)(tile_x * TILE_X) - q.gx, by = (float)(tile_y * TILE_Y) - q.gy;
   uint32_t m = 0u;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const float x0 = bx + 8.0f * (float)(s & 1), y0 = by + 8.0f * (float)(s >> 1);
-    if (!(rect_qmin(q, x0, x0 + 7.0f, y0, y0 + 7.0f) > q.tq)) m |= 1u << s;
+  for (int band = 0; band < 2; ++band) {
+    float lo, hi;
+    const float ya = by + 8.0f * (float)band;
+    if (!band_x_extent(q, ya, ya + 7.0f, lo, hi)) continue;
+#pragma unroll
+    for (int col = 0; col < 2; ++col) {
+      const float xa = bx + 8.0f * (float)col;
+      if (xa <= hi && xa + 7.0f >= lo) m |= 1u << (2 * band + col);
+    }
   }
   return m;
 }
@@ -386,6 +385,8 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
 int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,
                      int64_t N, hipStream_t s);
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);
+int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
+                       double* part, double* loss, int accumulate, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s);
 

@@ -15,12 +15,20 @@ namespace gslm {
 // round's hit bits in list order.  No block barrier: a wave leaves as soon as all of its pixels have stopped,
 // however far the tile's other quadrants still go (a block-cooperative version with 256-entry LDS batches
 // measured 1.5% slower on the full forward).
+// MODE (the epilogue): FWD_FULL colour + inverse depth + final_T / n_contrib (gslm_rasterize, the drop-in forward);
+// FWD_NO_INV the same without the inverse-depth accumulation (out_invdepth NULL: the LM paths); FWD_LOSS the
+// validation loss of the LM line search without any image: per pixel r = m clamp(C + T bg) - gt (gslm_lm_residual's
+// arithmetic), sum r^2 in double per tile -> part[tile] (gslm_rasterize_loss).
+enum { FWD_FULL = 0, FWD_NO_INV = 1, FWD_LOSS = 2 };
+
+template <int MODE>
 __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* __restrict__ ranges,
                                                           const uint32_t* __restrict__ tile_order,
                                                           const uint32_t* __restrict__ point_list,
                                                           const float4* __restrict__ rec, float* __restrict__ out_color,
                                                           float* __restrict__ out_invdepth, float* __restrict__ final_T,
-                                                          uint32_t* __restrict__ n_contrib) {
+                                                          uint32_t* __restrict__ n_contrib, const float* __restrict__ gt,
+                                                          const float* __restrict__ mask, double* __restrict__ part) {
   __shared__ float4 s_rec[4][3 * 64];
   const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -71,24 +79,57 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
           C0 += b.z * wt;
           C1 += b.w * wt;
           C2 += cc.x * wt;
-          Dp += cc.y * wt;
+          if (MODE == FWD_FULL) Dp += cc.y * wt;
           T = test_T;
-          last = (uint32_t)(base + j + 1);  // 1-based list position
+          if (MODE != FWD_LOSS) last = (uint32_t)(base + j + 1);  // 1-based list position
         }
       }
       if (__ballot(!done) == 0ull) break;
     }
     wave_lds_sync();
   }
-  if (inside) {
-    const int64_t pid = (int64_t)py * v.W + px;
-    const int64_t HW = (int64_t)v.H * v.W;
+  const int64_t pid = (int64_t)py * v.W + px;
+  const int64_t HW = (int64_t)v.H * v.W;
+  if constexpr (MODE == FWD_LOSS) {
+    __shared__ double s_sum[4];
+    double acc = 0.0;
+    if (inside) {
+      const float m = mask ? mask[pid] : 1.0f;
+      const float R[3] = {C0 + T * v.bg[0], C1 + T * v.bg[1], C2 + T * v.bg[2]};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float r = m * fminf(fmaxf(R[c], 0.0f), 1.0f) - gt[c * HW + pid];
+        acc += (double)r * (double)r;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0) s_sum[q] = acc;
+    __syncthreads();
+    if (tid == 0) part[tile] = ((s_sum[0] + s_sum[1]) + s_sum[2]) + s_sum[3];
+  } else if (inside) {
     final_T[pid] = T;
     n_contrib[pid] = last;
     out_color[pid] = C0 + T * v.bg[0];
     out_color[HW + pid] = C1 + T * v.bg[1];
     out_color[2 * HW + pid] = C2 + T * v.bg[2];
-    if (out_invdepth) out_invdepth[pid] = Dp;
+    if (MODE == FWD_FULL) out_invdepth[pid] = Dp;
+  }
+}
+
+// sum of the per-tile loss partials in tile order (deterministic), times 2 (the [r; r] aliasing)
+__global__ __launch_bounds__(256) void k_tile_loss_final(const double* __restrict__ part, int np, int accumulate,
+                                                          double* __restrict__ loss) {
+  __shared__ double s[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    *loss = accumulate ? *loss + l : l;
   }
 }
 
@@ -96,8 +137,29 @@ int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
                       float* out_invdepth, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) return GSLM_OK;
-  hipLaunchKernelGGL(k_render_fwd_wave, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order, bb.point_list,
-                     gb.rec, out_color, out_invdepth, ib.final_T, ib.n_contrib);
+  if (out_invdepth)
+    hipLaunchKernelGGL(k_render_fwd_wave<FWD_FULL>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, out_color, out_invdepth, ib.final_T, ib.n_contrib, (const float*)nullptr,
+                       (const float*)nullptr, (double*)nullptr);
+  else
+    hipLaunchKernelGGL(k_render_fwd_wave<FWD_NO_INV>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                       bb.point_list, gb.rec, out_color, (float*)nullptr, ib.final_T, ib.n_contrib, (const float*)nullptr,
+                       (const float*)nullptr, (double*)nullptr);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
+                       double* part, double* loss, int accumulate, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (ntiles == 0) {
+    if (!accumulate) GSLM_HIP_CHECK(hipMemsetAsync(loss, 0, sizeof(double), s));
+    return GSLM_OK;
+  }
+  hipLaunchKernelGGL(k_render_fwd_wave<FWD_LOSS>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+                     bb.point_list, gb.rec, (float*)nullptr, (float*)nullptr, (float*)nullptr, (uint32_t*)nullptr, gt,
+                     mask, part);
+  hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const double*)part, ntiles, accumulate, loss);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

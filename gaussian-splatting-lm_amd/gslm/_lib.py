@@ -94,6 +94,11 @@ EXPORTS = {
     "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_loss_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
+    "gslm_rasterize_loss": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32,
+                                           ctypes.c_void_p]),
     "gslm_forward": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -196,7 +201,10 @@ def _load():
         raise ImportError(f"libgslm.so not found at {LIB_PATH}: build it with "
                           f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
     lib = ctypes.CDLL(LIB_PATH)
+    ab_mode = os.environ.get("GSLM_ABI_ANY") == "1" and "GSLM_LIB" in os.environ and LIB_PATH != _DEFAULT_LIB
     for name, (restype, argtypes) in EXPORTS.items():
+        if ab_mode and not hasattr(lib, name):
+            continue  # an older A/B build without this entry point (only the A/B tools load those)
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes

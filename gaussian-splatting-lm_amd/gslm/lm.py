@@ -47,7 +47,9 @@ class ViewRaster:
         # product on the current geometry (GSLM_MV_TAIL_CLEAN): false after a forward or a backward
         self.tail_clean = False
 
-    def forward(self, g, stream):
+    def forward(self, g, stream, want_invdepth=True):
+        """The full forward (the drop-in's gslm_preprocess + gslm_rasterize).  want_invdepth=False: the LM paths,
+        which never read the inverse depth -- the blend then skips its accumulation (and its image)."""
         P = g.P
         dev = self.device
         self.tail_clean = False
@@ -67,7 +69,8 @@ class ViewRaster:
             self.binning = _lib.u8(int(need * 1.25) + 4096, dev)
         check(lib.gslm_rasterize(ctypes.byref(self.view), P, self.geom.data_ptr(), self.binning.data_ptr(),
                                  self.binning.numel(), self.N, self.image.data_ptr(), self.image.numel(),
-                                 self.color.data_ptr(), self.invdepth.data_ptr(), stream), "gslm_rasterize")
+                                 self.color.data_ptr(), self.invdepth.data_ptr() if want_invdepth else None, stream),
+              "gslm_rasterize")
         need = lib.gslm_scratch_bytes(P, self.N)
         if self.scratch is None or self.scratch.numel() < need:
             self.scratch = _lib.u8(int(need * 1.25) + 4096, dev)
@@ -128,7 +131,7 @@ class LMProblem:
         g = raw_gaussians(self.model)
         loss = torch.zeros((), dtype=torch.float64, device=self.device)
         for b, vr in enumerate(self.views):
-            R = vr.forward(g, self.stream)
+            R = vr.forward(g, self.stream, want_invdepth=False)
             if self.residuals[b] is None or self.residuals[b].shape != R.shape:
                 self.residuals[b] = torch.empty_like(R)
                 self.weights[b] = torch.empty_like(R)
@@ -744,8 +747,8 @@ class LossEvaluator:
     """The line search's validation loss: `val_loss_func().loss_scalar` of train_jvp.py:258,268,279 (batch_training_loss
     with disable_ssim=True over the validation views: 2 sum_b ||m_b clamp01(R_b) - gt_b||^2) on the HIP forward.
 
-    Per view: gslm_preprocess -> gslm_rasterize -> gslm_lm_residual in its loss-only form (no residual, weight or
-    seed images).  The depth order of each view depends on xyz alone, which the LM step freezes
+    Per view: gslm_preprocess_ordered -> gslm_rasterize_loss (binning, then the blend with the residual's loss
+    fused into its epilogue: no image is written).  The depth order of each view depends on xyz alone, which the LM step freezes
     (train_jvp.py:221-227): it is sorted at the first evaluation and reused by later ones while model._xyz is the
     same tensor at the same version (gslm_preprocess_ordered; the same point list, bitwise).  Views run in batches of `batch` workspaces: a batch's preprocesses are enqueued first and one
     gslm_num_rendered_many read-back sizes all their binnings (one host round trip per batch, not per view); the
@@ -768,19 +771,16 @@ class LossEvaluator:
                 raise ValueError("alpha mask must be [1, H, W]")
         self.stream = _lib.stream_handle(device)
         self.batch = max(1, min(int(batch), len(cams) or 1))
-        self.slots = [dict(geom=None, binning=None, image=None, color=None) for _ in range(self.batch)]
-        self.res_scratch = torch.empty(lib.gslm_residual_scratch_bytes(1, 1) // 8, dtype=torch.float64,
-                                       device=device)
+        self.slots = [dict(geom=None, binning=None) for _ in range(self.batch)]
+        nb = max([lib.gslm_loss_scratch_bytes(v.image_height, v.image_width) for v in self.views] + [8])
+        self.loss_scratch = torch.empty(nb // 8 + 1, dtype=torch.float64, device=device)
         self.num_rendered = [0] * len(cams)
         self._order_key, self._orders = None, [None] * len(cams)
 
-    def _slot(self, k, P, H, W):
+    def _slot(self, k, P):
         sl = self.slots[k]
         if sl["geom"] is None or sl["geom"].numel() < lib.gslm_geom_bytes(P):
             sl["geom"] = _lib.u8(lib.gslm_geom_bytes(P), self.device)
-        if sl["image"] is None or sl["image"].numel() < lib.gslm_image_bytes(H, W):
-            sl["image"] = _lib.u8(lib.gslm_image_bytes(H, W), self.device)
-            sl["color"] = torch.empty(3 * H * W, dtype=torch.float32, device=self.device)
         return sl
 
     def evaluate(self):
@@ -795,7 +795,7 @@ class LossEvaluator:
             self._order_key, self._orders = key, [None] * V
         for b0 in range(0, V, self.batch):
             idx = list(range(b0, min(V, b0 + self.batch)))
-            slots = [self._slot(k, P, self.views[i].image_height, self.views[i].image_width) for k, i in enumerate(idx)]
+            slots = [self._slot(k, P) for k in range(len(idx))]
             for sl, i in zip(slots, idx):
                 mode = 2 if self._orders[i] is not None else 1
                 if mode == 1:
@@ -814,14 +814,12 @@ class LossEvaluator:
                 need = lib.gslm_binning_bytes(N, H, W)
                 if sl["binning"] is None or sl["binning"].numel() < need:
                     sl["binning"] = _lib.u8(int(need * 1.25) + 4096, self.device)
-                check(lib.gslm_rasterize(ctypes.byref(vw), P, sl["geom"].data_ptr(), sl["binning"].data_ptr(),
-                                         sl["binning"].numel(), N, sl["image"].data_ptr(), sl["image"].numel(),
-                                         sl["color"].data_ptr(), None, self.stream), "gslm_rasterize")
                 m = self.masks[i]
-                check(lib.gslm_lm_residual(H, W, sl["color"].data_ptr(), self.gts[i].data_ptr(),
-                                           None if m is None else m.data_ptr(), None, None, None,
-                                           self.res_scratch.data_ptr(), self.res_scratch.numel() * 8,
-                                           loss.data_ptr(), int(i > 0), self.stream), "gslm_lm_residual")
+                check(lib.gslm_rasterize_loss(ctypes.byref(vw), P, sl["geom"].data_ptr(), sl["binning"].data_ptr(),
+                                              sl["binning"].numel(), N, self.gts[i].data_ptr(),
+                                              None if m is None else m.data_ptr(), self.loss_scratch.data_ptr(),
+                                              self.loss_scratch.numel() * 8, loss.data_ptr(), int(i > 0), self.stream),
+                      "gslm_rasterize_loss")
         if self.reduce is not None:
             self.reduce(loss)
         return loss

@@ -130,6 +130,16 @@ int gslm_num_rendered_many(const void* const* geoms, const int64_t* Ps, int32_t 
 int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
                    int64_t num_rendered, void* image, size_t image_bytes, float* out_color,
                    float* out_invdepth, void* stream);
+/* The LM line search's validation loss of one view with no image written (gslm.lm.LossEvaluator; train_jvp.py:258,
+ * 268,279 val_loss_func().loss_scalar with disable_ssim=True): gslm_rasterize's binning and blend, the blend's
+ * epilogue computing r = m clamp(color, 0, 1) - gt per pixel and channel (gslm_lm_residual's arithmetic; gt [3,H,W],
+ * alpha_mask [H,W] or NULL) and summing r^2 in double per tile, then *loss_dev = [*loss_dev if accumulate] +
+ * 2 sum over tiles in tile order (deterministic).  No colour, inverse depth, final_T or n_contrib is written.
+ * scratch >= gslm_loss_scratch_bytes(H, W). */
+size_t gslm_loss_scratch_bytes(int32_t H, int32_t W);
+int gslm_rasterize_loss(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                        int64_t num_rendered, const float* gt, const float* alpha_mask, void* scratch,
+                        size_t scratch_bytes, double* loss_dev, int32_t accumulate, void* stream);
 /* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
  * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
  * gslm_rasterize with a larger buffer). */

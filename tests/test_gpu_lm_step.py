@@ -143,8 +143,9 @@ def test_device_stopping_tests_equal_host(sched, kw):
 
 
 def test_loss_evaluator_equals_lmproblem_evaluate():
-    """The line search's loss-only evaluator (batched preprocesses, one num_rendered read-back per batch, the
-    residual kernel without its images) gives the bitwise same loss as LMProblem.evaluate over the same views."""
+    """The line search's loss-only evaluator (batched preprocesses, one num_rendered read-back per batch, the loss
+    fused into the blend's epilogue: gslm_rasterize_loss) gives LMProblem.evaluate's loss over the same views (the
+    same float residuals; only the double sum's order differs: 1e-12)."""
     from gslm.cameras import orbit_cameras
     from gslm.lm import LMProblem, LossEvaluator
     from gslm.model import synthetic_gaussians
@@ -153,17 +154,21 @@ def test_loss_evaluator_equals_lmproblem_evaluate():
     cams = orbit_cameras(5, 56, 40, seed=7, images=gts)
     for c in cams:
         c.to("cuda")
+    def close(a, b):
+        return abs(float(a) - float(b)) <= 1e-12 * abs(float(b))
+
     ref = float(LMProblem(m, cams, torch.zeros(3)).evaluate())
     for batch in (1, 2, 8):
         ev = LossEvaluator(m, cams, torch.zeros(3), batch=batch)
-        assert float(ev.evaluate()) == ref
-        assert float(ev.evaluate()) == ref  # reused workspaces and the cached depth orders (gslm_preprocess_ordered)
+        first = float(ev.evaluate())
+        assert close(first, ref)
+        assert float(ev.evaluate()) == first  # reused workspaces and the cached depth orders (gslm_preprocess_ordered)
     # a line-search-like step on everything but xyz: the cached orders stay valid (same point lists, bitwise)
     with torch.no_grad():
         m._opacity.add_(0.7 * torch.randn(m._opacity.shape, generator=torch.Generator().manual_seed(5)).cuda())
         m._scaling.add_(0.3 * torch.randn(m._scaling.shape, generator=torch.Generator().manual_seed(6)).cuda())
-    assert float(ev.evaluate()) == float(LMProblem(m, cams, torch.zeros(3)).evaluate())
+    assert close(ev.evaluate(), LMProblem(m, cams, torch.zeros(3)).evaluate())
     # xyz moves: the evaluator notices (tensor version) and sorts again
     with torch.no_grad():
         m._xyz.add_(0.05 * torch.randn(m._xyz.shape, generator=torch.Generator().manual_seed(7)).cuda())
-    assert float(ev.evaluate()) == float(LMProblem(m, cams, torch.zeros(3)).evaluate())
+    assert close(ev.evaluate(), LMProblem(m, cams, torch.zeros(3)).evaluate())
