@@ -747,15 +747,19 @@ class LossEvaluator:
     """The line search's validation loss: `val_loss_func().loss_scalar` of train_jvp.py:258,268,279 (batch_training_loss
     with disable_ssim=True over the validation views: 2 sum_b ||m_b clamp01(R_b) - gt_b||^2) on the HIP forward.
 
-    Per view: gslm_preprocess_ordered -> gslm_rasterize_loss (binning, then the blend with the residual's loss
-    fused into its epilogue: no image is written).  The depth order of each view depends on xyz alone, which the LM step freezes
-    (train_jvp.py:221-227): it is sorted at the first evaluation and reused by later ones while model._xyz is the
-    same tensor at the same version (gslm_preprocess_ordered; the same point list, bitwise).  Views run in batches of `batch` workspaces: a batch's preprocesses are enqueued first and one
-    gslm_num_rendered_many read-back sizes all their binnings (one host round trip per batch, not per view); the
-    loss accumulates in a device double, in view order.  `reduce`: a callable summing the device double over the
-    ranks that hold the other views (the multi-GPU line search, gslm.parallel.allreduce_loss)."""
+    Per view: gslm_preprocess_ordered -> gslm_rasterize_loss (binning, then the blend with the residual's loss fused
+    into its epilogue: no image is written).
+      * Depth order: it depends on xyz alone, which the LM step freezes (train_jvp.py:221-227), so each view's order
+        is sorted at its first evaluation and reused while model._xyz is the same tensor at the same version (the
+        same point list, bitwise).
+      * Batches: views run in batches of `batch` workspaces; a batch's preprocesses are enqueued first and one
+        gslm_num_rendered_many read-back sizes all their binnings (one host round trip per batch, not per view).
+      * Streams: consecutive views of a batch run on `streams` HIP streams, so one view's short serial kernels
+        (scans, the tile launch order, the loss reduction) and its blend's tail overlap another view's work.
+    Each view's loss lands in its own device double; the total is their sum (view order fixed, so run to run the
+    same).  `reduce`: a callable summing it over the ranks that hold the other views (gslm.parallel.allreduce_loss)."""
 
-    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None):
+    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None, streams=2):
         self.model = model
         self.device = device
         self.reduce = reduce
@@ -769,11 +773,12 @@ class LossEvaluator:
                 raise ValueError(f"ground truth must be float32 (3, {H}, {W}), got {gt.dtype} {tuple(gt.shape)}")
             if m is not None and m.numel() != H * W:
                 raise ValueError("alpha mask must be [1, H, W]")
-        self.stream = _lib.stream_handle(device)
         self.batch = max(1, min(int(batch), len(cams) or 1))
+        nstr = max(1, min(int(streams), self.batch))
+        self.streams = [torch.cuda.Stream(device) for _ in range(nstr)] if nstr > 1 else [None]
         self.slots = [dict(geom=None, binning=None) for _ in range(self.batch)]
         nb = max([lib.gslm_loss_scratch_bytes(v.image_height, v.image_width) for v in self.views] + [8])
-        self.loss_scratch = torch.empty(nb // 8 + 1, dtype=torch.float64, device=device)
+        self.loss_scratch = [torch.empty(nb // 8 + 1, dtype=torch.float64, device=device) for _ in self.streams]
         self.num_rendered = [0] * len(cams)
         self._order_key, self._orders = None, [None] * len(cams)
 
@@ -783,43 +788,64 @@ class LossEvaluator:
             sl["geom"] = _lib.u8(lib.gslm_geom_bytes(P), self.device)
         return sl
 
+    def _stream(self, k):
+        """(torch stream or None, hipStream_t) of batch position k."""
+        st = self.streams[k % len(self.streams)]
+        return st, (st.cuda_stream if st is not None else _lib.stream_handle(self.device))
+
     def evaluate(self):
         """Device double: the loss over this evaluator's views (summed over the ranks with `reduce`)."""
         g = raw_gaussians(self.model)
         P = g.P
-        loss = torch.zeros((), dtype=torch.float64, device=self.device)
         V = len(self.views)
+        losses = torch.zeros(max(V, 1), dtype=torch.float64, device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        main_h = main.cuda_stream
         xyz = self.model._xyz
         key = (xyz.data_ptr(), xyz._version, P)
         if key != self._order_key:  # xyz moved: sort again
             self._order_key, self._orders = key, [None] * V
+        for st in self.streams:  # the parameters (and the zeroed losses) as the main stream left them
+            if st is not None:
+                st.wait_stream(main)
         for b0 in range(0, V, self.batch):
             idx = list(range(b0, min(V, b0 + self.batch)))
             slots = [self._slot(k, P) for k in range(len(idx))]
-            for sl, i in zip(slots, idx):
+            for k, (sl, i) in enumerate(zip(slots, idx)):
                 mode = 2 if self._orders[i] is not None else 1
                 if mode == 1:
                     self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                _, sh = self._stream(k)
                 check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(g), sl["geom"].data_ptr(),
-                                                  sl["geom"].numel(), None, self._orders[i].data_ptr(), mode,
-                                                  self.stream), "gslm_preprocess_ordered")
+                                                  sl["geom"].numel(), None, self._orders[i].data_ptr(), mode, sh),
+                      "gslm_preprocess_ordered")
+            for st in self.streams:
+                if st is not None:
+                    main.wait_stream(st)
             geoms = (ctypes.c_void_p * len(idx))(*[sl["geom"].data_ptr() for sl in slots])
             Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
             Ns = (ctypes.c_int64 * len(idx))()
-            check(lib.gslm_num_rendered_many(geoms, Ps, len(idx), Ns, self.stream), "gslm_num_rendered_many")
+            check(lib.gslm_num_rendered_many(geoms, Ps, len(idx), Ns, main_h), "gslm_num_rendered_many")
             for k, (sl, i) in enumerate(zip(slots, idx)):
                 vw = self.views[i]
                 H, W, N = vw.image_height, vw.image_width, int(Ns[k])
                 self.num_rendered[i] = N
+                st, sh = self._stream(k)
                 need = lib.gslm_binning_bytes(N, H, W)
                 if sl["binning"] is None or sl["binning"].numel() < need:
+                    if sl["binning"] is not None and st is not None:
+                        main.wait_stream(st)  # the old buffer is freed on the main stream: after its last use
                     sl["binning"] = _lib.u8(int(need * 1.25) + 4096, self.device)
                 m = self.masks[i]
+                scr = self.loss_scratch[k % len(self.streams)]
                 check(lib.gslm_rasterize_loss(ctypes.byref(vw), P, sl["geom"].data_ptr(), sl["binning"].data_ptr(),
                                               sl["binning"].numel(), N, self.gts[i].data_ptr(),
-                                              None if m is None else m.data_ptr(), self.loss_scratch.data_ptr(),
-                                              self.loss_scratch.numel() * 8, loss.data_ptr(), int(i > 0), self.stream),
-                      "gslm_rasterize_loss")
+                                              None if m is None else m.data_ptr(), scr.data_ptr(), scr.numel() * 8,
+                                              losses.data_ptr() + 8 * i, 0, sh), "gslm_rasterize_loss")
+        for st in self.streams:
+            if st is not None:
+                main.wait_stream(st)
+        loss = losses[:V].sum() if V else losses[0]
         if self.reduce is not None:
             self.reduce(loss)
         return loss
