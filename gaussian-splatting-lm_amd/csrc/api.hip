@@ -148,20 +148,23 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
     GSLM_HIP_CHECK(hipMemsetAsync(gb.counters, 0, 4, s));
     return GSLM_OK;
   }
+  const uint32_t* tiles_sorted = nullptr;  // the tile counts in depth order, when the sort gathered them
   if (order_mode == 2) {
     GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
   } else {
-    // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass)
+    // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass), the last writes
+    // tiles[index] where the sorted keys would go
     bool alt = false;
-    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true);
+    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true, gb.tiles);
     if (st) return st;
     if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+    tiles_sorted = alt ? gb.keys_alt : gb.depth_key;
     if (order_mode == 1)
       GSLM_HIP_CHECK(hipMemcpyAsync(depth_order, gb.sorted_idx, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
   }
   // tile-count scans in index order (gradient-row offsets goff) and in depth order (duplicate offsets)
   return exclusive_scan_u32_dual(gb.tiles, gb.sorted_idx, gb.goff, gb.offsets, P, gb.scan_tmp, gb.counters + 1,
-                                 gb.counters, s);
+                                 gb.counters, s, tiles_sorted);
 }
 
 }  // namespace gslm

@@ -62,6 +62,74 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   if (radii_out) radii_out[i] = o.radius;
 }
 
+// k_preprocess with the block's SH-rest rows staged by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction,
+// no VGPR round trip) and the staging overlapped with the geometry: every thread loads its Gaussian's geometry
+// inputs first (and waits for them), the waves then issue the block's DMA chunks, run the geometry arithmetic
+// (cull, EWA, conic, radius, rect) while the rows land, and meet at one barrier before the colour.  The register
+// path (k_preprocess<_, true>) keeps one 16-B load per thread in flight per round trip of its staging loop.
+// Same arithmetic in the same order: bitwise the same records.
+__device__ __forceinline__ void glds16(const float4* src, float4* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <bool RAW>
+__global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float4* __restrict__ rec,
+                                                         uint32_t* __restrict__ depth_key,
+                                                         uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
+                                                         uint32_t* __restrict__ clampw, int* __restrict__ radii_out) {
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];  // [256 * rest_stride]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + tid;
+  const bool live = i < g.P;
+  // 1. this Gaussian's geometry inputs, waited for before any DMA is in flight (hipcc waits vmcnt(0) at the first
+  //    use of an ordinary load issued while an LDS-DMA is outstanding)
+  PreIn in{};
+  if (live) load_pre_in<RAW>(g, i, in);
+  asm volatile("" : : "v"(in.x), "v"(in.y), "v"(in.z), "v"(in.c[0]), "v"(in.c[1]), "v"(in.c[2]), "v"(in.c[3]),
+               "v"(in.c[4]), "v"(in.c[5]), "v"(in.qw), "v"(in.op));
+  // 2. the block's SH-rest rows, [nv][rest_stride] floats, contiguous in the leaf: 64-float4 chunks per wave
+  const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+  const int64_t total = nv * g.rest_stride;  // i0 * rest_stride * 4 B is 16-B aligned (i0 % 256 == 0)
+  const int64_t n4 = total / 4;
+  const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+  float4* dst4 = reinterpret_cast<float4*>(s_sh);
+  for (int64_t c = w; c * 64 < n4; c += 4) {
+    const int64_t e = min(c * 64 + lane, n4 - 1);  // past the rows: re-read the last float4 (its slot is unused)
+    glds16(src4 + e, dst4 + c * 64);
+  }
+  // 3. the geometry while the rows land
+  PreOut o;
+  o.depth = 0.f;
+  const bool vis = live && preprocess_core<RAW, false>(v, g, i, in, o);
+  // 4. the DMA landed (the barrier's vmcnt(0)); a row tail that is not a whole float4 (last block only) by plain loads
+  __syncthreads();
+  if (n4 * 4 < total) {
+    for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+    __syncthreads();
+  }
+  if (!live) return;
+  tiles[i] = 0u;
+  depth_key[i] = 0xFFFFFFFFu;
+  if (radii_out) radii_out[i] = 0;
+  if (o.depth > 0.2f) depth_key[i] = __float_as_uint(o.depth);  // as k_preprocess: every Gaussian before the near plane
+  if (!vis) return;
+  g.rest = s_sh;
+  g.rest_base = i0;
+  preprocess_color(v, g, i, in, o);
+  const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
+  const float4 r1 = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
+  const float4 r2 = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.tq);
+  rec[RECS * i + 0] = r0;
+  rec[RECS * i + 1] = r1;
+  rec[RECS * i + 2] = r2;
+  tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
+  rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  clampw[i] = o.clamped;
+  if (radii_out) radii_out[i] = o.radius;
+}
+
 // One block per 256 consecutive Gaussians of the depth order: their (tile, id) pairs are one contiguous
 // output range, written by the whole block in element order (coalesced, and a large Gaussian's tiles are
 // spread over the block instead of one thread's loop).  Element e belongs to the last Gaussian whose
@@ -223,6 +291,13 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
 }
 
 // ------------------------------------------------------------------ launchers
+// k_preprocess_dma (default) or the register-staged k_preprocess: GSLM_PREPROCESS_STAGING=reg selects the latter
+// (an A/B switch; both write the bitwise same records)
+static const bool g_preprocess_dma = [] {
+  const char* e = getenv("GSLM_PREPROCESS_STAGING");
+  return !(e && e[0] == 'r');
+}();
+
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   const int nb = (int)((g.P + 255) / 256);
@@ -230,7 +305,13 @@ int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* 
   const bool stage = !g.colors && g.rest && g.M > 1 && g.rest_stride == 3 * (g.M - 1) &&
                      ((uintptr_t)g.rest & 15u) == 0;
   const size_t lds = stage ? (size_t)256 * g.rest_stride * sizeof(float) : 0;
-  if (g.raw && stage)
+  if (g.raw && stage && g_preprocess_dma)
+    hipLaunchKernelGGL((k_preprocess_dma<true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, gb.clampw, radii_out);
+  else if (stage && g_preprocess_dma)
+    hipLaunchKernelGGL((k_preprocess_dma<false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
+                       gb.rect, gb.clampw, radii_out);
+  else if (g.raw && stage)
     hipLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
                        gb.rect, gb.clampw, radii_out);
   else if (g.raw)

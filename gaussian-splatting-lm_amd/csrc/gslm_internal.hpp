@@ -56,8 +56,10 @@ inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_b
 
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
 // ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
+// last_gather (or NULL): the last pass writes last_gather[value] in place of each sorted key.
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
-                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false);
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false,
+                     const uint32_t* last_gather = nullptr);
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;
@@ -71,8 +73,10 @@ inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n)
 // out[i] = sum_{j<i} in[idx ? idx[j] : j];  *total (device) = full sum.
 int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
                        uint32_t* total, hipStream_t s);
-// out_a[i] = sum_{j<i} in[j], out_b[i] = sum_{j<i} in[idx[j]] in one pass (tmp: scan_tmp_bytes(n)).
+// out_a[i] = sum_{j<i} in[j], out_b[i] = sum_{j<i} b[j] in one pass (tmp: scan_tmp_bytes(n)), b = in_b, or in
+// gathered through idx when in_b is NULL.
 int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* out_a, uint32_t* out_b, int64_t n,
-                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s);
+                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s,
+                            const uint32_t* in_b = nullptr);
 
 }  // namespace gslm

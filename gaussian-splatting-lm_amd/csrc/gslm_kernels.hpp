@@ -241,10 +241,61 @@ __device__ __forceinline__ void load_scale_rot(const GaussK& g, int64_t i, float
   }
 }
 
-// SURVEY Appendix A steps 1-9 for one Gaussian; returns false when culled.
+// The per-Gaussian inputs of the preprocess, loaded apart from its arithmetic (k_preprocess_dma loads them before
+// it issues the SH-rest LDS-DMA, so the arithmetic runs while that lands).
+struct PreIn {
+  float x, y, z;
+  float c[6];  // cov3D_precomp, or (s0 s1 s2 | q0 q1 q2 q3 in c[3..5] and qw) -- see load_pre_in
+  float qw;
+  float op;
+};
+
 template <bool RAW>
-__device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, int64_t i, PreOut& o) {
-  const float x = g.means3D[3 * i + 0], y = g.means3D[3 * i + 1], z = g.means3D[3 * i + 2];
+__device__ __forceinline__ void load_pre_in(const GaussK& g, int64_t i, PreIn& in) {
+  in.x = g.means3D[3 * i + 0];
+  in.y = g.means3D[3 * i + 1];
+  in.z = g.means3D[3 * i + 2];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) in.c[k] = g.cov3D[6 * i + k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) in.c[k] = g.scales[3 * i + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) in.c[3 + k] = g.rot[4 * i + k];
+    in.qw = g.rot[4 * i + 3];
+  }
+  in.op = g.opac[i];
+}
+
+// Step 8 (colour) of one Gaussian: colors_precomp, or SH (utils/sh_utils.py:57-112) -> max(result + 0.5, 0) with
+// the clamp mask (gaussian_renderer/__init__.py:79-80).
+__device__ __forceinline__ void preprocess_color(const ViewK& v, const GaussK& g, int64_t i, const PreIn& in, PreOut& o) {
+  o.clamped = 0u;
+  if (g.colors) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.rgb[k] = g.colors[3 * i + k];
+  } else {
+    float dx = in.x - v.campos[0], dy = in.y - v.campos[1], dz = in.z - v.campos[2];
+    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    auto shf = [&](int k, int ch) { return g.sh(i, k, ch); };
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float r = sh_color(v.D, dx, dy, dz, shf, ch);
+      if (r < 0.0f) o.clamped |= (1u << ch);
+      o.rgb[ch] = fmaxf(r, 0.0f);
+    }
+  }
+}
+
+// SURVEY Appendix A steps 1-9 for one Gaussian from its loaded inputs; returns false when culled.  COLOR = false
+// leaves o.rgb / o.clamped to preprocess_color (the SH-rest rows not yet staged).
+template <bool RAW, bool COLOR>
+__device__ __forceinline__ bool preprocess_core(const ViewK& v, const GaussK& g, int64_t i, const PreIn& in, PreOut& o) {
+  const float x = in.x, y = in.y, z = in.z;
   const float tz = tp_row(v.view, x, y, z, 2);
   o.depth = tz;  // set before any cull: the depth order of every Gaussian in front of the near plane
   if (!(tz > 0.2f)) return false;
@@ -256,10 +307,20 @@ __device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, 
   float c[6];
   if (g.cov3D) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) c[k] = g.cov3D[6 * i + k];
+    for (int k = 0; k < 6; ++k) c[k] = in.c[k];
   } else {
     float s[3], q[4], R[9];
-    load_scale_rot<RAW>(g, i, s, q);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] = RAW ? expf(in.c[k]) : in.c[k];
+    q[0] = in.c[3];
+    q[1] = in.c[4];
+    q[2] = in.c[5];
+    q[3] = in.qw;
+    if (RAW) {  // load_scale_rot's normalisation (gaussian_model.py:198)
+      const float nrm = fmaxf(sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]), 1e-12f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = q[k] / nrm;
+    }
     quat_rot(q[0], q[1], q[2], q[3], R);
     cov3d_from(v.scale_mod * s[0], v.scale_mod * s[1], v.scale_mod * s[2], R, c);
   }
@@ -290,30 +351,20 @@ __device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, 
   o.rmax_y = min(v.gy, max(0, trunc_i((((o.y + radius) + 16.0f) - 1.0f) / 16.0f)));
   if ((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y) == 0) return false;
 
-  o.clamped = 0u;
-  if (g.colors) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o.rgb[k] = g.colors[3 * i + k];
-  } else {
-    float dx = x - v.campos[0], dy = y - v.campos[1], dz = z - v.campos[2];
-    const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
-    dx = dx / len;
-    dy = dy / len;
-    dz = dz / len;
-    auto shf = [&](int k, int ch) { return g.sh(i, k, ch); };
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      const float r = sh_color(v.D, dx, dy, dz, shf, ch);
-      if (r < 0.0f) o.clamped |= (1u << ch);
-      o.rgb[ch] = fmaxf(r, 0.0f);
-    }
-  }
-  const float op = RAW ? sigmoidf_(g.opac[i]) : g.opac[i];
+  if (COLOR) preprocess_color(v, g, i, in, o);
+  const float op = RAW ? sigmoidf_(in.op) : in.op;
   o.opac = op * h;
   o.depth = tz;
   o.radius = (int)radius;
   o.tq = v.exhaustive ? INFINITY : alpha_threshold(o.opac);  // INFINITY: every quadrant visited
   return true;
+}
+
+template <bool RAW>
+__device__ __forceinline__ bool preprocess_one(const ViewK& v, const GaussK& g, int64_t i, PreOut& o) {
+  PreIn in;
+  load_pre_in<RAW>(g, i, in);
+  return preprocess_core<RAW, true>(v, g, i, in, o);
 }
 
 // ---------------- workspace views ----------------

@@ -96,7 +96,7 @@ template <int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
-    const uint32_t* __restrict__ totals) {
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather) {
   static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
   constexpr int TILE = SORT_THREADS * ITEMS;
   constexpr int WAVE_KEYS = TILE / 4;
@@ -178,8 +178,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t k = s_keys[e];
     const uint32_t d = (k >> shift) & dmask;
     const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_loc[d]);
-    kout[pos] = k;
-    vout[pos] = s_vals[e];
+    const uint32_t val = s_vals[e];
+    // kgather (the last pass of the depth sort): the sorted keys are not needed afterwards, so their slot carries
+    // kgather[value] in sorted order instead (the tile counts the depth-order scan reads, gathered once here)
+    kout[pos] = kgather ? kgather[val] : k;
+    vout[pos] = val;
   }
 }
 
@@ -271,8 +274,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __r
 
 // Two exclusive scans of the same counts in one pass: in index order (out_a) and gathered through idx
 // (out_b).  block_sums holds 2 nb partials: [0, nb) for a, [nb, 2 nb) for b.
+// in_b (or NULL: in gathered through idx) is the second sequence
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_reduce(const uint32_t* __restrict__ in,
-                                                               const uint32_t* __restrict__ idx, int64_t n,
+                                                               const uint32_t* __restrict__ idx,
+                                                               const uint32_t* __restrict__ in_b, int64_t n,
                                                                uint32_t* __restrict__ block_sums) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_reduce(const uint32_t* _
     const int64_t i = base + k;
     if (i < n) {
       acc_a += in[i];
-      acc_b += in[idx[i]];
+      acc_b += in_b ? in_b[i] : in[idx[i]];
     }
   }
   uint32_t tot_a, tot_b;
@@ -314,7 +319,8 @@ __global__ __launch_bounds__(256) void k_scan2_top(uint32_t* __restrict__ block_
 }
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __restrict__ in,
-                                                              const uint32_t* __restrict__ idx, int64_t n,
+                                                              const uint32_t* __restrict__ idx,
+                                                              const uint32_t* __restrict__ in_b, int64_t n,
                                                               const uint32_t* __restrict__ block_sums,
                                                               uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b) {
   __shared__ uint32_t s_w[4];
@@ -326,7 +332,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const int64_t i = base + k;
     va[k] = i < n ? in[i] : 0u;
-    vb[k] = i < n ? in[idx[i]] : 0u;
+    vb[k] = i < n ? (in_b ? in_b[i] : in[idx[i]]) : 0u;
     acc_a += va[k];
     acc_b += vb[k];
   }
@@ -350,22 +356,22 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __
 }  // namespace
 
 int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* out_a, uint32_t* out_b, int64_t n,
-                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s) {
+                            uint32_t* tmp, uint32_t* total_a, uint32_t* total_b, hipStream_t s, const uint32_t* in_b) {
   if (n <= 0) {
     GSLM_HIP_CHECK(hipMemsetAsync(total_a, 0, 4, s));
     GSLM_HIP_CHECK(hipMemsetAsync(total_b, 0, 4, s));
     return GSLM_OK;
   }
   const int nb = (int)scan_blocks(n);
-  hipLaunchKernelGGL(k_scan2_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
+  hipLaunchKernelGGL(k_scan2_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp);
   hipLaunchKernelGGL(k_scan2_top, dim3(2), dim3(256), 0, s, tmp, nb, total_a, total_b);
-  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out_a, out_b);
+  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
 
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
-                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values) {
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values, const uint32_t* last_gather) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const int nb = (int)sort_blocks(n);
@@ -382,16 +388,17 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
     const int nbits = end_bit - shift < per ? end_bit - shift : per;  // digit bits of this pass
     const uint32_t dmask = (1u << nbits) - 1u;
     const uint32_t* vin = (first && iota_values) ? (const uint32_t*)nullptr : vi;
+    const uint32_t* kg = (shift + per >= end_bit) ? last_gather : nullptr;  // the last pass
     if (small) {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
       hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift,
-                         nbits, hist, nb, totals);
+                         nbits, hist, nb, totals, kg);
     } else {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
       hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift, nbits,
-                         hist, nb, totals);
+                         hist, nb, totals, kg);
     }
     first = false;
     GSLM_LAUNCH_CHECK();
