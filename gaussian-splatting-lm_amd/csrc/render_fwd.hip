@@ -46,8 +46,9 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
   float T = 1.0f;
   uint32_t last = 0;
   float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+  uint64_t dmask = __builtin_amdgcn_ballot_w64(done);  // lanes stopped (or outside the image), wave-uniform
   for (int base = 0; base < n; base += 64) {
-    if (__ballot(!done) == 0ull) break;  // every pixel of this quadrant has stopped
+    if (dmask == ~0ull) break;  // every pixel of this quadrant has stopped
     const int k = base + lane;
     bool hit = false;
     if (k < n) {
@@ -71,20 +72,21 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float alpha = fminf(0.99f, b.y * gexp(power));
       const float test_T = T * (1.0f - alpha);
-      if (!done && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
-        if (test_T < 0.0001f) {
-          done = true;
-        } else {
-          const float wt = alpha * T;
-          C0 += b.z * wt;
-          C1 += b.w * wt;
-          C2 += cc.x * wt;
-          if (MODE == FWD_FULL) Dp += cc.y * wt;
-          T = test_T;
-          if (MODE != FWD_LOSS) last = (uint32_t)(base + j + 1);  // 1-based list position
-        }
-      }
-      if (__ballot(!done) == 0ull) break;
+      // branch-free visit: a lane that does not blend adds colour * 0 (+-0 leaves every sum unchanged bitwise: they
+      // start at +0 and colours, 1/depth are >= 0) and keeps T; the per-lane state stays in lane masks, no exec juggling
+      const bool live = !done && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
+      const bool stop = live && test_T < 0.0001f;
+      const bool blend = live && !stop;
+      done = done || stop;
+      const float wt = blend ? alpha * T : 0.0f;
+      C0 += b.z * wt;
+      C1 += b.w * wt;
+      C2 += cc.x * wt;
+      if (MODE == FWD_FULL) Dp += cc.y * wt;
+      T = blend ? test_T : T;
+      if (MODE != FWD_LOSS) last = blend ? (uint32_t)(base + j + 1) : last;  // 1-based list position
+      dmask |= __builtin_amdgcn_ballot_w64(stop);  // the stop compare's lane mask, no VGPR round trip
+      if (dmask == ~0ull) break;
     }
     wave_lds_sync();
   }
