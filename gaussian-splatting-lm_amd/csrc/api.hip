@@ -456,6 +456,10 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
   if (!b.g.raw) { set_error("matvec: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   b.v.stop = opts ? opts->cg_ctl : nullptr;
+  if (opts && opts->rest_basis) {
+    set_error("matvec: rest_basis is an option of gslm_tangent_views / gslm_gather_screen");
+    return GSLM_ERR_INVALID;
+  }
   const bool proj = opts && (opts->flags & GSLM_MV_SH_REST_PROJECTED) && b.g.M > 1;
   GaussK t = tangent_from_grads(vin, b.g, mask_xyz != 0);
   if (proj) {
@@ -550,6 +554,70 @@ int gslm_sh_rest_project(const gslm_view* view, const gslm_gaussians* gi, int32_
   return launch_sh_rest_project(v, g, mode, in, in_stride, out, out_stride, (hipStream_t)stream);
 }
 
+// the views of one SH-rest coordinate system: 1..GSLM_MAX_REST_VIEWS, one SH degree
+static int rest_views(const char* who, const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, ViewK* vk,
+                      GaussK* g) {
+  if (!views || !gi || nviews < 1 || nviews > GSLM_MAX_REST_VIEWS) {
+    set_error(std::string(who) + ": NULL views / gaussians or nviews outside 1..GSLM_MAX_REST_VIEWS");
+    return GSLM_ERR_INVALID;
+  }
+  int st;
+  for (int b = 0; b < nviews; ++b) {
+    if ((st = make_view(&views[b], gi->max_coeffs, &vk[b]))) return st;
+    if (vk[b].D != vk[0].D) {
+      set_error(std::string(who) + ": the views must share one SH degree");
+      return GSLM_ERR_INVALID;
+    }
+  }
+  if ((st = make_gauss(gi, &vk[0], g, false))) return st;
+  if (g->P > 0 && !g->means3D) {
+    set_error(std::string(who) + ": NULL means3D");
+    return GSLM_ERR_INVALID;
+  }
+  return GSLM_OK;
+}
+
+int gslm_rest_basis(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, float* R_out, void* stream) {
+  ViewK vk[GSLM_MAX_REST_VIEWS];
+  GaussK g;
+  int st;
+  if ((st = rest_views("rest_basis", views, nviews, gi, vk, &g))) return st;
+  if (g.P > 0 && !R_out) { set_error("rest_basis: NULL R_out"); return GSLM_ERR_INVALID; }
+  return launch_rest_basis(vk, nviews, g, R_out, (hipStream_t)stream);
+}
+
+int gslm_rest_coords(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, const float* R, int32_t mode,
+                     const float* in, int64_t in_stride, float* out, int64_t out_stride, void* stream) {
+  ViewK vk[GSLM_MAX_REST_VIEWS];
+  GaussK g;
+  int st;
+  if ((st = rest_views("rest_coords", views, nviews, gi, vk, &g))) return st;
+  if (mode != 0 && mode != 1) { set_error("rest_coords: mode must be 0 (expand) or 1 (project)"); return GSLM_ERR_INVALID; }
+  if (g.M < 2) return GSLM_OK;
+  if (g.P > 0 && (!R || !in || !out)) { set_error("rest_coords: NULL buffer"); return GSLM_ERR_INVALID; }
+  const int64_t full = 3 * (int64_t)(g.M - 1), coords = 3 * (int64_t)nviews;
+  if ((mode == 0 && (in_stride < coords || out_stride < full)) || (mode == 1 && (in_stride < full || out_stride < coords))) {
+    set_error("rest_coords: strides too small for [P,V,3] / [P,M-1,3] rows");
+    return GSLM_ERR_INVALID;
+  }
+  return launch_rest_coords(vk, nviews, g, R, mode, in, in_stride, out, out_stride, (hipStream_t)stream);
+}
+
+// opts->rest_basis of gslm_tangent_views / gslm_gather_screen: the coordinate system and this call's columns
+static int rest_opts(const char* who, const gslm_matvec_opts* opts, int32_t nviews, RestK* rc) {
+  *rc = RestK{};
+  if (!opts || !opts->rest_basis) return GSLM_OK;
+  if (opts->rest_views < 1 || opts->rest_views > GSLM_MAX_REST_VIEWS || opts->view_base < 0 ||
+      opts->view_base + nviews > opts->rest_views) {
+    set_error(std::string(who) + ": rest_views outside 1..GSLM_MAX_REST_VIEWS or views past its last column");
+    return GSLM_ERR_INVALID;
+  }
+  rc->R = opts->rest_basis;
+  rc->V = opts->rest_views;
+  rc->view_base = opts->view_base;
+  return GSLM_OK;
+}
+
 int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, const float* screen,
                        const gslm_grads* vin, const gslm_grads* y, const gslm_matvec_opts* opts, void* stream) {
   if (!views || nviews < 1 || nviews > 16 || !gi || !screen || !vin || !y) {
@@ -573,8 +641,10 @@ int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussi
   double* part = dot_out ? (double*)opts->dot_scratch : nullptr;
   const int64_t sstride = (opts && opts->screen_stride) ? opts->screen_stride : g.P;
   if (sstride < g.P) { set_error("gather_screen: screen_stride below P"); return GSLM_ERR_INVALID; }
+  RestK rc;
+  if ((st = rest_opts("gather_screen", opts, nviews, &rc))) return st;
   if ((st = launch_gather_screen(vk, nviews, g, screen, sstride, make_gradk(y), make_gradk(vin), damp7,
-                                 (stages & GSLM_STAGE_OVERWRITE) != 0, part, (hipStream_t)stream)))
+                                 (stages & GSLM_STAGE_OVERWRITE) != 0, part, (hipStream_t)stream, rc)))
     return st;
   if (dot_out) return gslm_dot_finalize(part, (int32_t)((g.P + 255) / 256), dot_out, stream);
   return GSLM_OK;
@@ -609,16 +679,23 @@ int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussi
     return GSLM_ERR_INVALID;
   }
   GaussK t = tangent_from_grads(vin, g, mask_xyz != 0);
-  const int R = 3 * (g.M - 1);
+  RestK rc;
+  if ((st = rest_opts("tangent_views", opts, nviews, &rc))) return st;
+  const int R = rc.R ? 3 * rc.V : 3 * (g.M - 1);
   if (t.rest && t.rest_stride != R) {
-    set_error("tangent_views: the SH-rest tangent needs stride 3(M-1)");
+    set_error(rc.R ? "tangent_views: SH-rest coordinates need stride 3 rest_views"
+                   : "tangent_views: the SH-rest tangent needs stride 3(M-1)");
     return GSLM_ERR_INVALID;
+  }
+  if (rc.R && g.M > 1) {
+    t.rest_R = rc.R;
+    t.rest_V = rc.V;
   }
   XpbyK xp{};
   const bool fused = opts && opts->xpby_s;
   if (fused && (st = build_xpby(opts, vin, R, mask_xyz != 0, &xp))) return st;
   return launch_tangent_views(vk, nviews, g, t, vflags, flags_stride, trec_out, trec_stride, fused ? &xp : nullptr,
-                              (hipStream_t)stream, mask_xyz != 0);
+                              (hipStream_t)stream, mask_xyz != 0, rc.view_base);
 }
 
 int gslm_matvec_view(const gslm_view* view, const gslm_gaussians* gi, const gslm_grads* vin,

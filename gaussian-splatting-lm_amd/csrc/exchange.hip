@@ -37,9 +37,12 @@ __global__ __launch_bounds__(256) void k_rowsum_screen(int64_t P, const uint32_t
   out[2 * i + 1] = make_float4(G2[6], G2[7], G2[8], __uint_as_float(flags));
 }
 
+// COORDS: the SH-rest group in gslm_rest_basis coordinates -- view b's rest gradient B_rest(dir_b) (x) dres_b adds
+// R[j][view_base + b] dres_b to coordinate j (j <= view_base + b), accumulated in dsh[1 + j]; nothing else changes.
+template <bool COORDS>
 __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, const float4* __restrict__ screen,
-                                                        int64_t sstride, FlatK o) {
-  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
+                                                        int64_t sstride, FlatK o, RestK rc) {
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * rest width]
   __shared__ double s_dot[4];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   ChainOut acc;
@@ -65,11 +68,25 @@ __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, cons
       for (int k = 0; k < 3; ++k) acc.dscale[k] += co.dscale[k];
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc.drot[k] += co.drot[k];
+      if constexpr (COORDS) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        acc.dsh[k][0] += co.dsh[k][0];
-        acc.dsh[k][1] += co.dsh[k][1];
-        acc.dsh[k][2] += co.dsh[k][2];
+        for (int ch = 0; ch < 3; ++ch) acc.dsh[0][ch] += co.dsh[0][ch];
+        const int col = rc.view_base + b;
+        const float* Rc = rc.R + i * rest_basis_floats(rc.V) + rest_basis_floats(col);
+#pragma unroll
+        for (int j = 0; j < MAX_REST_VIEWS; ++j)
+          if (j <= col) {
+            const float r = Rc[j];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) acc.dsh[1 + j][ch] += r * co.dres[ch];
+          }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          acc.dsh[k][0] += co.dsh[k][0];
+          acc.dsh[k][1] += co.dsh[k][1];
+          acc.dsh[k][2] += co.dsh[k][2];
+        }
       }
     }
   }
@@ -86,10 +103,10 @@ int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs&
 
 int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, int64_t sstride,
                          const GradK& y, const GradK& vin, const double* damp7, bool overwrite, double* dot_part,
-                         hipStream_t s) {
+                         hipStream_t s, const RestK& rc) {
   if (g.P == 0) return GSLM_OK;
   FlatK o;
-  const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o);
+  const int st = make_flatk(g, y, vin, damp7, overwrite, dot_part, &o, false, rc.R ? rc.V : 0);
   if (st) return st;
   if (nviews < 1 || nviews > MAX_SCREEN_VIEWS) {
     set_error("gather_screen: 1..16 views per call");
@@ -98,9 +115,15 @@ int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const 
   ViewsK vs;
   for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
   vs.n = nviews;
-  const size_t lds = sh_stage_floats<false>(g.M) * sizeof(float) + 16;
-  hipLaunchKernelGGL(k_gather_screen, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, vs, g,
-                     reinterpret_cast<const float4*>(screen), sstride, o);
+  const unsigned nb = (unsigned)((g.P + 255) / 256);
+  const float4* sc = reinterpret_cast<const float4*>(screen);
+  if (o.rest_V) {
+    const size_t lds = (size_t)256 * 3 * o.rest_V * sizeof(float) + 16;
+    hipLaunchKernelGGL(k_gather_screen<true>, dim3(nb), dim3(256), lds, s, vs, g, sc, sstride, o, rc);
+  } else {
+    const size_t lds = sh_stage_floats<false>(g.M) * sizeof(float) + 16;
+    hipLaunchKernelGGL(k_gather_screen<false>, dim3(nb), dim3(256), lds, s, vs, g, sc, sstride, o, rc);
+  }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -117,6 +140,153 @@ __global__ __launch_bounds__(256) void k_view_flags(int64_t P, const uint32_t* _
 int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s) {
   if (P == 0) return GSLM_OK;
   hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, gb.clampw, gb.tiles, out);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+}  // namespace gslm
+
+namespace gslm {
+
+// ---------------------------------------------------------------- SH-rest coordinates (gslm_rest_basis)
+// The SH-rest basis vector of view v at Gaussian i: B[k], k = 1..nc-1, the fp32 values chain_jvp / chain_vjp use
+// (same direction arithmetic as chain_eval).
+__device__ __forceinline__ void rest_basis_vec(const ViewK& v, const float* __restrict__ m, int64_t i, float B[16]) {
+  const float dx = m[3 * i + 0] - v.campos[0], dy = m[3 * i + 1] - v.campos[1], dz = m[3 * i + 2] - v.campos[2];
+  const float len = sqrtf((dx * dx + dy * dy) + dz * dz);
+  sh_basis(v.D, dx / len, dy / len, dz / len, B);
+}
+
+__device__ __forceinline__ double rest_gram(const float A[16], const float B[16], int nc) {
+  double acc = 0.0;
+  for (int k = 1; k < nc; ++k) acc += (double)A[k] * (double)B[k];
+  return acc;
+}
+
+// One thread per Gaussian: the Gram matrix G[a][b] = <B_a, B_b> of the V views' SH-rest vectors (double), its
+// upper Cholesky factor column by column (G = R^T R, i.e. Gram-Schmidt of B_0, B_1, .. in view order), a view
+// adding less than 1e-6 of its norm to the earlier ones' span dropped (row zeroed), R packed by columns.
+__global__ __launch_bounds__(256) void k_rest_basis(ViewsK vs, GaussK g, float* __restrict__ R) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.P) return;
+  const int V = vs.n, nc = (vs.v[0].D + 1) * (vs.v[0].D + 1);
+  double Rm[MAX_REST_VIEWS][MAX_REST_VIEWS];
+  float* out = R + i * rest_basis_floats(V);
+#pragma unroll
+  for (int b = 0; b < MAX_REST_VIEWS; ++b) {
+    if (b >= V) break;
+    float Bb[16], Ba[16];
+    rest_basis_vec(vs.v[b], g.means3D, i, Bb);
+    double Gc[MAX_REST_VIEWS];
+#pragma unroll
+    for (int a = 0; a < MAX_REST_VIEWS; ++a)
+      if (a < b) {
+        rest_basis_vec(vs.v[a], g.means3D, i, Ba);
+        Gc[a] = rest_gram(Ba, Bb, nc);
+      }
+    const double gbb = rest_gram(Bb, Bb, nc);
+    double d = gbb;
+#pragma unroll
+    for (int j = 0; j < MAX_REST_VIEWS; ++j)
+      if (j < b) {
+        double r = 0.0;
+        if (Rm[j][j] != 0.0) {
+          r = Gc[j];
+#pragma unroll
+          for (int q = 0; q < MAX_REST_VIEWS; ++q)
+            if (q < j) r -= Rm[q][j] * Rm[q][b];
+          r /= Rm[j][j];
+        }
+        Rm[j][b] = r;
+        d -= r * r;
+      }
+    Rm[b][b] = (gbb > 0.0 && d > 1e-12 * gbb) ? sqrt(d) : 0.0;
+#pragma unroll
+    for (int j = 0; j < MAX_REST_VIEWS; ++j)
+      if (j <= b) out[rest_basis_floats(b) + j] = (float)Rm[j][b];
+  }
+}
+
+// mode 0 (expand): t = Q c = B_K R_KK^-1 c over the kept views K (back substitution); mode 1 (project):
+// c = Q^T t = R_KK^-T B_K^T t (forward substitution).  One thread per Gaussian, double arithmetic.
+__global__ __launch_bounds__(256) void k_rest_coords(ViewsK vs, GaussK g, const float* __restrict__ R, int mode,
+                                                     const float* __restrict__ in, int64_t in_stride,
+                                                     float* __restrict__ out, int64_t out_stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.P) return;
+  const int V = vs.n, nc = (vs.v[0].D + 1) * (vs.v[0].D + 1), M = g.M;
+  const float* Rp = R + i * rest_basis_floats(V);
+  auto Rjb = [&](int j, int b) { return (double)Rp[rest_basis_floats(b) + j]; };
+  double y[MAX_REST_VIEWS][3];
+  float B[16];
+  if (mode == 0) {
+#pragma unroll
+    for (int b = MAX_REST_VIEWS - 1; b >= 0; --b) {
+      if (b >= V) continue;
+      const double rbb = Rjb(b, b);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        double acc = in[i * in_stride + 3 * b + ch];
+#pragma unroll
+        for (int j = 0; j < MAX_REST_VIEWS; ++j)
+          if (j > b && j < V) acc -= Rjb(b, j) * y[j][ch];
+        y[b][ch] = rbb != 0.0 ? acc / rbb : 0.0;
+      }
+    }
+    double t[15][3];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) t[k][0] = t[k][1] = t[k][2] = 0.0;
+#pragma unroll
+    for (int b = 0; b < MAX_REST_VIEWS; ++b) {
+      if (b >= V) break;
+      rest_basis_vec(vs.v[b], g.means3D, i, B);
+#pragma unroll
+      for (int k = 1; k < 16; ++k)
+        if (k < nc)
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) t[k - 1][ch] += (double)B[k] * y[b][ch];
+    }
+    for (int k = 1; k < M; ++k)
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) out[i * out_stride + 3 * (k - 1) + ch] = k < nc ? (float)t[k - 1][ch] : 0.f;
+  } else {
+#pragma unroll
+    for (int b = 0; b < MAX_REST_VIEWS; ++b) {
+      if (b >= V) break;
+      rest_basis_vec(vs.v[b], g.means3D, i, B);
+      const double rbb = Rjb(b, b);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        double z = 0.0;
+        for (int k = 1; k < nc && k < M; ++k) z += (double)B[k] * (double)in[i * in_stride + 3 * (k - 1) + ch];
+#pragma unroll
+        for (int j = 0; j < MAX_REST_VIEWS; ++j)
+          if (j < b) z -= Rjb(j, b) * y[j][ch];
+        y[b][ch] = rbb != 0.0 ? z / rbb : 0.0;
+        out[i * out_stride + 3 * b + ch] = (float)y[b][ch];
+      }
+    }
+  }
+}
+
+int launch_rest_basis(const ViewK* views, int nviews, const GaussK& g, float* R, hipStream_t s) {
+  if (g.P == 0) return GSLM_OK;
+  ViewsK vs;
+  for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
+  vs.n = nviews;
+  hipLaunchKernelGGL(k_rest_basis, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, vs, g, R);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_rest_coords(const ViewK* views, int nviews, const GaussK& g, const float* R, int mode, const float* in,
+                       int64_t in_stride, float* out, int64_t out_stride, hipStream_t s) {
+  if (g.P == 0) return GSLM_OK;
+  ViewsK vs;
+  for (int b = 0; b < nviews; ++b) vs.v[b] = views[b];
+  vs.n = nviews;
+  hipLaunchKernelGGL(k_rest_coords, dim3((unsigned)((g.P + 255) / 256)), dim3(256), 0, s, vs, g, R, mode, in, in_stride,
+                     out, out_stride);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -470,7 +470,22 @@ __device__ __forceinline__ void chain_jvp(const ViewK& v, const GaussK& g, const
     if (t.dc) {
       float B[16];
       sh_basis(v.D, e.dir[0], e.dir[1], e.dir[2], B);
-      if (t.rest_proj) {
+      if (t.rest_R) {
+        // SH-rest coordinates c_j in the orthonormal basis Q of span{B_rest(dir_b)}: B_rest(dir)^T Q c = sum_j R[j][col] c_j
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) dres[ch] += B[0] * t.sh(i, 0, ch);
+        if (t.rest && nc > 1) {
+          const float* Rc = t.rest_R + i * rest_basis_floats(t.rest_V) + rest_basis_floats(t.rest_col);
+          const float* c = t.rest + (i - t.rest_base) * t.rest_stride;
+#pragma unroll
+          for (int j = 0; j < MAX_REST_VIEWS; ++j)
+            if (j <= t.rest_col) {
+              const float r = Rc[j];
+#pragma unroll
+              for (int ch = 0; ch < 3; ++ch) dres[ch] += r * c[3 * j + ch];
+            }
+        }
+      } else if (t.rest_proj) {
         // projected SH-rest tangent: sum_k B_k v_k = |B_rest| c for v = (B_rest / |B_rest|) (x) c
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) dres[ch] += B[0] * t.sh(i, 0, ch);

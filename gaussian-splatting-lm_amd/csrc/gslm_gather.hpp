@@ -14,6 +14,7 @@ struct FlatK {
   int use_damp;
   int overwrite;
   int rest_proj;      // GSLM_MV_SH_REST_PROJECTED: the rest group is 3 floats per Gaussian (see chain_jvp)
+  int rest_V;         // SH-rest coordinates (gslm_rest_basis): the rest group is 3 rest_V floats, staged from dsh[1..V]
   double* dot_part;   // per-block partials of <v, y> over the written elements (NULL = off)
 };
 
@@ -72,14 +73,18 @@ __device__ __forceinline__ double store_group(float* y, float d, int use_damp, i
 
 // FlatK over a flat param-space output y and input v (GradK views of the 7-group vectors).
 inline int make_flatk(const GaussK& g, const GradK& y, const GradK& vin, const double* damp7, bool overwrite,
-                      double* dot_part, FlatK* out, bool rest_proj = false) {
-  const int64_t R = rest_proj ? 3 : 3 * (g.M - 1);
+                      double* dot_part, FlatK* out, bool rest_proj = false, int rest_V = 0) {
+  const int64_t R = rest_V ? 3 * rest_V : rest_proj ? 3 : 3 * (g.M - 1);
   if (g.cov3D || g.colors || !g.raw || (g.M > 1 && y.rest_stride != R) || y.dc_stride != 3) {
     set_error("LM gather expects raw leaves with SH colours and a flat param-space output");
     return GSLM_ERR_INVALID;
   }
   if (rest_proj && g.M > 1 && vin.rest && vin.rest_stride != 3) {
     set_error("LM gather: a projected SH-rest group has 3 floats per Gaussian in v and y");
+    return GSLM_ERR_INVALID;
+  }
+  if (rest_V && g.M > 1 && vin.rest && vin.rest_stride != R) {
+    set_error("LM gather: SH-rest coordinates need 3 rest_views floats per Gaussian in v and y");
     return GSLM_ERR_INVALID;
   }
   FlatK o;
@@ -90,6 +95,7 @@ inline int make_flatk(const GaussK& g, const GradK& y, const GradK& vin, const d
   o.use_damp = damp7 ? 1 : 0;
   o.overwrite = overwrite ? 1 : 0;
   o.rest_proj = (rest_proj && g.M > 1) ? 1 : 0;
+  o.rest_V = g.M > 1 ? rest_V : 0;
   o.dot_part = dot_part;
   if (o.use_damp || dot_part)
     for (int k = 0; k < 6; ++k)
@@ -123,7 +129,7 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
   const int64_t i = i0 + tid;
   const int64_t nvalid = min((int64_t)blockDim.x, g.P - i0);
   // a projected SH-rest group is a 3-wide group of its own below; the LDS-staged stream covers none
-  const int R = o.rest_proj ? 0 : 3 * (g.M - 1);
+  const int R = o.rest_proj ? 0 : o.rest_V ? 3 * o.rest_V : 3 * (g.M - 1);
   const bool dot = o.dot_part != nullptr;
   const int u = o.use_damp, ow = o.overwrite;
   const bool need_v = u || dot;
@@ -158,6 +164,14 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) val[ch] = nb * co.dres[ch];
       dacc += store_group<3>(o.y[2], o.damp[2], u, 3 * i, ow, dot, val, vp, yp);
+    } else if (o.rest_V) {
+      // SH-rest coordinates: dsh[1 + j] holds coordinate j's gradient (k_gather_screen<true>)
+#pragma unroll
+      for (int j = 0; j < MAX_REST_VIEWS; ++j)
+        if (j < o.rest_V) {
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) s_rest[tid * R + 3 * j + ch] = co.dsh[1 + j][ch];
+        }
     } else if (FACTORED) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) s_rest[tid * SHB_STRIDE + k] = co.shB[k];

@@ -23,6 +23,12 @@ struct GaussK {
   // tangents only (GSLM_MV_SH_REST_PROJECTED): rest holds 3 floats per Gaussian, the coordinates of the
   // SH-rest tangent along the unit basis direction B_rest(dir) / |B_rest(dir)| of this view
   int rest_proj = 0;
+  // tangents only, the Gaussian-sharded exchange's SH-rest coordinates (gslm_rest_basis): rest holds 3 rest_V
+  // floats per Gaussian, rest_R the Gaussians' packed factors R (rest_V (rest_V + 1) / 2 floats each) and
+  // rest_col this view's column of R
+  const float* rest_R = nullptr;
+  int rest_V = 0;
+  int rest_col = 0;
   __device__ __forceinline__ float sh(int64_t i, int k, int c) const {
     return k == 0 ? dc[i * dc_stride + c] : rest[(i - rest_base) * rest_stride + 3 * (k - 1) + c];
   }
@@ -473,16 +479,29 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
                        const ScratchBufs& sb, const XpbyK* xp, hipStream_t s, bool compact);
 int launch_rowsum_screen(const GaussK& g, const GeomBufs& gb, const ScratchBufs& sb, float* out, hipStream_t s);
 constexpr int MAX_SCREEN_VIEWS = 16;
+constexpr int MAX_REST_VIEWS = GSLM_MAX_REST_VIEWS;
+// packed upper-triangular factor R of gslm_rest_basis: column b starts at b (b + 1) / 2
+__host__ __device__ constexpr int rest_basis_floats(int V) { return V * (V + 1) / 2; }
+// SH-rest coordinates for launch_gather_screen (nullptr R: the full [M-1][3] layout)
+struct RestK {
+  const float* R = nullptr;
+  int V = 0;
+  int view_base = 0;
+};
 struct ViewsK {
   ViewK v[MAX_SCREEN_VIEWS];
   int n;
 };
 int launch_gather_screen(const ViewK* views, int nviews, const GaussK& g, const float* screen, int64_t sstride,
                          const GradK& y, const GradK& vin, const double* damp7, bool overwrite, double* dot_part,
-                         hipStream_t s);
+                         hipStream_t s, const RestK& rc = RestK{});
+int launch_rest_basis(const ViewK* views, int nviews, const GaussK& g, float* R, hipStream_t s);
+int launch_rest_coords(const ViewK* views, int nviews, const GaussK& g, const float* R, int mode, const float* in,
+                       int64_t in_stride, float* out, int64_t out_stride, hipStream_t s);
 int launch_view_flags(int64_t P, const GeomBufs& gb, uint32_t* out, hipStream_t s);
 int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
-                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact);
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact,
+                         int view_base = 0);
 int launch_jvp(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,
                const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb, float* out_color_t, float* out_inv_t,
                hipStream_t s);

@@ -165,7 +165,7 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
 template <bool XPBY>
 __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, GaussK t, const uint32_t* __restrict__ vflags,
                                                         int64_t fstride, float4* __restrict__ out, int64_t ostride,
-                                                        XpbyK xp, int compact) {
+                                                        XpbyK xp, int compact, int view_base) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + threadIdx.x;
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, Gaus
   for (int b = 0; b < vs.n; ++b) {
     const uint32_t f = vflags[(int64_t)b * fstride + i];
     if (!(f >> 31)) continue;
+    t.rest_col = view_base + b;  // SH-rest coordinates: this view's column of R
     float T2[10];
     chain_jvp<true>(vs.v[b], g, t, nullptr, i, f & 7u, T2);
     store_trec(out, (int64_t)b * ostride + i, T2, compact != 0);
@@ -193,7 +194,8 @@ __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, Gaus
 }
 
 int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const GaussK& t, const uint32_t* vflags,
-                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact) {
+                         int64_t fstride, float* out, int64_t ostride, const XpbyK* xp, hipStream_t s, bool compact,
+                         int view_base) {
   if (nviews < 1 || nviews > MAX_SCREEN_VIEWS) {
     set_error("tangent_views: 1..16 views per call");
     return GSLM_ERR_INVALID;
@@ -212,10 +214,10 @@ int launch_tangent_views(const ViewK* views, int nviews, const GaussK& g, const 
   float4* o = reinterpret_cast<float4*>(out);
   if (xp)
     hipLaunchKernelGGL(k_tangent_views<true>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, *xp,
-                       compact ? 1 : 0);
+                       compact ? 1 : 0, view_base);
   else
     hipLaunchKernelGGL(k_tangent_views<false>, dim3(nb), dim3(256), lds, s, vs, g, t, vflags, fstride, o, ostride, none,
-                       compact ? 1 : 0);
+                       compact ? 1 : 0, view_base);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

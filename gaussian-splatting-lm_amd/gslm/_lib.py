@@ -17,6 +17,7 @@ GSLM_OK = 0
 GSLM_ERR_INVALID = -1
 GSLM_ERR_HIP = -2
 GSLM_ERR_CAPACITY = -3
+GSLM_MAX_REST_VIEWS = 8  # include/gslm.h
 
 
 class GslmView(ctypes.Structure):
@@ -62,6 +63,7 @@ class GslmMatvecOpts(ctypes.Structure):
         ("alpha_num", ctypes.c_void_p), ("alpha_den", ctypes.c_void_p), ("xpby_x_offset", ctypes.c_int64),
         ("trec_in", ctypes.c_void_p), ("screen_stride", ctypes.c_int64),
         ("cg_ctl", ctypes.c_void_p),
+        ("rest_basis", ctypes.c_void_p), ("rest_views", ctypes.c_int32), ("view_base", ctypes.c_int32),
     ]
 
 
@@ -124,6 +126,11 @@ EXPORTS = {
     "gslm_sh_rest_project": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_int32,
                                             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                             ctypes.c_void_p]),
+    "gslm_rest_basis": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
+                                       ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_rest_coords": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
+                                        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "gslm_gather_screen": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
                                           ctypes.c_void_p, ctypes.POINTER(GslmGrads), ctypes.POINTER(GslmGrads),
                                           ctypes.c_void_p, ctypes.c_void_p]),
@@ -189,7 +196,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 5  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 6  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):

@@ -254,12 +254,21 @@ class GaussianShardedOperator:
         self.S = max(1, -(-self.P // n))
         self.lo = min(self.rank * self.S, self.P)
         self.hi = min(self.lo + self.S, self.P)
-        # the exposure group (zero in every LM iterate: J has no exposure column) lives on rank 0
-        self.layout = ParamLayout(self.hi - self.lo, full.K, full.n_exposure if self.rank == 0 else 0)
         self.mask_xyz = getattr(local, "mask_xyz", True)
         self.device = getattr(local, "device", "cpu")
         self.kernel_path = hasattr(local, "views") and all_cams is not None
         self.all_cams = all_cams
+        # SH-rest coordinates (gslm_rest_basis): with V <= GSLM_MAX_REST_VIEWS views in the job every CG iterate's
+        # SH-rest group lies in the span of the V views' SH-rest directions, 3 V floats per Gaussian instead of
+        # 3(K-1) in the shard's vectors (GSLM_SHARD_REST=full keeps the reference's layout)
+        V = len(all_cams) if self.kernel_path else 0
+        from gslm._lib import GSLM_MAX_REST_VIEWS
+        self.rest_views = V if (full.K > 1 and 0 < V <= GSLM_MAX_REST_VIEWS and 3 * V < 3 * (full.K - 1)
+                                and os.environ.get("GSLM_SHARD_REST", "coords") != "full") else 0
+        self._rest_R = None  # [S][V (V + 1) / 2] factors, per geometry (evaluate)
+        # the exposure group (zero in every LM iterate: J has no exposure column) lives on rank 0
+        self.layout = ParamLayout(self.hi - self.lo, full.K, full.n_exposure if self.rank == 0 else 0,
+                                  rest_views=self.rest_views)
         if self.kernel_path:
             self.per = len(local.views)
             if self.per < 1 or len(all_cams) != n * self.per:
@@ -309,8 +318,37 @@ class GaussianShardedOperator:
     def _group_rows(self, layout, vec):
         return {name: t.reshape(t.shape[0], math.prod(t.shape[1:])) for name, t in layout.views(vec).items()}
 
+    # ------------------------------------------------------------------ SH-rest coordinates
+    def _rest_args(self):
+        from gslm import _lib
+        from gslm.params import raw_gaussians
+        gs = _slice_gaussians(raw_gaussians(self.local.model), self.lo, self.hi)
+        vptr = ctypes.cast(ctypes.byref(self.views_kt, 0), ctypes.POINTER(_lib.GslmView))
+        return gs, vptr
+
+    def rest_basis(self):
+        """gslm_rest_basis of this shard's Gaussians over the job's views (recomputed per geometry)."""
+        if self._rest_R is None:
+            from gslm._lib import check, lib
+            V, S = self.rest_views, self.hi - self.lo
+            self._rest_R = torch.zeros(max(1, S * V * (V + 1) // 2), dtype=torch.float32, device=self.device)
+            gs, vptr = self._rest_args()
+            check(lib.gslm_rest_basis(vptr, V, ctypes.byref(gs), self._rest_R.data_ptr(), self.local.stream),
+                  "gslm_rest_basis")
+        return self._rest_R
+
+    def _rest_convert(self, mode, src, dst):
+        """mode 0: coordinates [S][V][3] -> the reference's [S][K-1][3] rows; 1: the reverse (projection)."""
+        from gslm._lib import check, lib
+        if self.hi == self.lo:
+            return
+        R = self.rest_basis()
+        gs, vptr = self._rest_args()
+        check(lib.gslm_rest_coords(vptr, self.rest_views, ctypes.byref(gs), R.data_ptr(), mode, src.data_ptr(),
+                                   src.shape[1], dst.data_ptr(), dst.shape[1], self.local.stream), "gslm_rest_coords")
+
     def shard(self, full_vec, out=None):
-        """This rank's shard of a full-layout vector."""
+        """This rank's shard of a full-layout vector (SH-rest coordinates: its projection onto the views' span)."""
         out = self.zeros() if out is None else out
         src = self._group_rows(self.full_layout, full_vec)
         dst = self._group_rows(self.layout, out)
@@ -318,6 +356,9 @@ class GaussianShardedOperator:
             if name == "exposure":
                 if self.layout.n_exposure:
                     dst[name].copy_(src[name])
+                continue
+            if name == "features_rest" and self.rest_views:
+                self._rest_convert(1, src[name][self.lo:self.hi].contiguous(), dst[name])
                 continue
             dst[name].copy_(src[name][self.lo:self.hi])
         return out
@@ -328,6 +369,10 @@ class GaussianShardedOperator:
         n, S = self.world_size, self.S
         names = [g for g in GROUPS if g != "exposure"]
         rows = self._group_rows(self.layout, vec)
+        if self.rest_views:
+            full_rest = torch.zeros(self.hi - self.lo, 3 * (self.full_layout.K - 1), dtype=vec.dtype, device=vec.device)
+            self._rest_convert(0, rows["features_rest"], full_rest)
+            rows["features_rest"] = full_rest
         widths = [math.prod(self.full_layout.shapes[g][1:]) for g in names]
         F = sum(widths)
         pack = torch.zeros(S, F, dtype=vec.dtype, device=vec.device)
@@ -372,6 +417,7 @@ class GaussianShardedOperator:
         self.local.loss = loss
         if self.kernel_path:
             self._exchange_flags()
+            self._rest_R = None  # the geometry (xyz) may have changed: SH-rest factors recomputed on first use
         return loss
 
     def rhs(self, out):
@@ -500,12 +546,16 @@ class GaussianShardedOperator:
             # shard never holds (rank 0 owns Gaussians whenever P > 0)
             pre = None
         # 1. tangent records of this shard for every view (direction update fused into the first call)
+        R = self.rest_basis() if self.rest_views else None
         for c0 in range(0, nv, chunk):
             c1 = min(nv, c0 + chunk)
             opts = None
-            if pre is not None and c0 == 0:
+            if (pre is not None and c0 == 0) or R is not None:
                 opts = _lib.GslmMatvecOpts()
+            if pre is not None and c0 == 0:
                 keep.append(self._pre_opts(opts, v, pre))
+            if R is not None:
+                opts.rest_basis, opts.rest_views, opts.view_base = R.data_ptr(), self.rest_views, c0
             vptr = ctypes.cast(ctypes.byref(self.views_kt, c0 * vsz), ctypes.POINTER(_lib.GslmView))
             check(lib.gslm_tangent_views(vptr, c1 - c0, ctypes.byref(gs), ctypes.byref(vs), int(self.mask_xyz),
                                          b["flags"].data_ptr() + 4 * c0 * S, S,
@@ -543,6 +593,8 @@ class GaussianShardedOperator:
             opts.stages = 7 | (8 if c0 == 0 else 0)
             opts.damp7 = self._damps if c0 == 0 else None
             opts.screen_stride = S
+            if R is not None:
+                opts.rest_basis, opts.rest_views, opts.view_base = R.data_ptr(), self.rest_views, c0
             if fuse and c1 == nv:
                 opts.dot_vy = dot_out
                 opts.dot_scratch = loc.dot_scratch.data_ptr()

@@ -13,13 +13,19 @@ GROUPS = ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity
 
 class ParamLayout:
     """rest_projected: the SH-rest group holds 3 floats per Gaussian -- its coordinates along one view's unit
-    basis direction (GSLM_MV_SH_REST_PROJECTED, gslm_sh_rest_project) -- instead of 3(K-1)."""
+    basis direction (GSLM_MV_SH_REST_PROJECTED, gslm_sh_rest_project) -- instead of 3(K-1).
+    rest_views = V > 0: the SH-rest group holds 3 V floats per Gaussian, its coordinates in an orthonormal basis
+    of the V views' SH-rest directions (the Gaussian-sharded exchange, gslm_rest_basis / gslm_rest_coords)."""
 
-    def __init__(self, P, sh_coeffs, n_exposure=1, rest_projected=False):
+    def __init__(self, P, sh_coeffs, n_exposure=1, rest_projected=False, rest_views=0):
         self.P, self.K, self.n_exposure = int(P), int(sh_coeffs), int(n_exposure)
         K = self.K
         self.rest_projected = bool(rest_projected) and K > 1
-        rest_rows = 1 if self.rest_projected else K - 1
+        self.rest_views = int(rest_views) if K > 1 else 0
+        if self.rest_projected and self.rest_views:
+            raise ValueError("rest_projected and rest_views are exclusive")
+        rest_rows = self.rest_views or (1 if self.rest_projected else K - 1)
+        self.rest_rows = rest_rows
         self.shapes = {
             "xyz": (P, 3), "features_dc": (P, 1, 3), "features_rest": (P, rest_rows, 3), "scaling": (P, 3),
             "rotation": (P, 4), "opacity": (P, 1), "exposure": (n_exposure, 3, 4)}
@@ -34,8 +40,9 @@ class ParamLayout:
 
     @property
     def floats_per_gaussian(self):
-        """F = 11 + 3K: xyz 3, dc 3, rest 3(K-1), scaling 3, rotation 4, opacity 1 (17 when projected)."""
-        return 17 if self.rest_projected else 11 + 3 * self.K
+        """F = 11 + 3K: xyz 3, dc 3, rest 3(K-1), scaling 3, rotation 4, opacity 1 (17 when projected, 14 + 3V
+        in rest_views coordinates)."""
+        return 14 + 3 * self.rest_rows if self.K > 1 else 14
 
     def views(self, flat):
         """dict group -> view of the flat tensor with the reference shape."""
@@ -74,7 +81,7 @@ class ParamLayout:
         g.sh_dc = base + f * self.offsets["features_dc"][0]
         g.sh_dc_stride = 3
         g.sh_rest = (base + f * self.offsets["features_rest"][0]) if self.K > 1 else None
-        g.sh_rest_stride = 3 if self.rest_projected else 3 * (self.K - 1)
+        g.sh_rest_stride = 3 * self.rest_rows
         g.colors = None
         g.accumulate = int(bool(accumulate))
         return g

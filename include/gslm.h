@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 5
+#define GSLM_ABI_VERSION 6
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -244,6 +244,14 @@ typedef struct gslm_matvec_opts {
    * the dot or the direction update), so a host can enqueue a whole CGLS schedule without reading the tests
    * back each iteration. */
   const double* cg_ctl;
+  /* gslm_tangent_views / gslm_gather_screen only (ABI 6): SH-rest coordinates of the Gaussian-sharded exchange.
+   * When rest_basis is set, the SH-rest group of v, y (and of the fused direction update's s) holds 3 rest_views
+   * floats per Gaussian -- the coordinates of the SH-rest vector in an orthonormal basis of span{B_rest(dir_b)}
+   * over the job's rest_views views b -- and rest_basis is gslm_rest_basis' per-Gaussian factor R of those
+   * views; view k of this call is column view_base + k of R.  See gslm_rest_basis. */
+  const float* rest_basis;
+  int32_t rest_views;
+  int32_t view_base;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
@@ -298,6 +306,27 @@ int gslm_view_flags(const void* geom, int64_t P, uint32_t* out, void* stream);
 int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const gslm_grads* v,
                        int32_t mask_xyz, const uint32_t* vflags, int64_t flags_stride, float* trec_out,
                        int64_t trec_stride, const gslm_matvec_opts* opts, void* stream);
+
+/* ---- SH-rest coordinates of the Gaussian-sharded exchange (ABI 6) ----
+ * The SH-rest column of J for view b is B_rest(dir_b) (x) (d rgb), B_rest the view's SH basis over
+ * coefficients 1..nc-1.  So with V views every CGLS iterate started from J^T b keeps each Gaussian's SH-rest
+ * group in span{B_rest(dir_b) : b < V} (x) R^3, which (J^T J + D) maps into itself (D is a scalar on the group):
+ * 3 V coordinates per Gaussian in an orthonormal basis Q of that span replace 3(M-1) floats (V = 1 is
+ * GSLM_MV_SH_REST_PROJECTED).  With B = Q R (Gram-Schmidt in view order; R upper triangular, the Cholesky
+ * factor of the Gram matrix B^T B, computed in double), view b's colour tangent is sum_{j<=b} R[j][b] c_j and
+ * its gradient adds R[j][b] dL/drgb_b to coordinate j: the per-Gaussian kernels need R only.  A view whose
+ * direction adds less than 1e-6 of its norm to the span of the earlier ones (R[b][b]^2 <= 1e-12 G[b][b]) gets
+ * row b of R zeroed: its coordinate stays 0.
+ *   gslm_rest_basis   R_out[i * V(V+1)/2 + b(b+1)/2 + j] = R[j][b] (j <= b), float, for the V = nviews views
+ *                     (1..GSLM_MAX_REST_VIEWS) and the Gaussians of g (means3D and max_coeffs used; the SH
+ *                     degree of views[0]).
+ *   gslm_rest_coords  mode 0 (expand): out[i*out_stride + 3(k-1) + c] = (Q c_i)[k][c] (0 for k >= nc);
+ *                     mode 1 (project): out[i*out_stride + 3j + c] = (Q^T t_i)[j][c], t_i = in[i*in_stride ..]
+ *                     in the [M-1][3] layout (the orthogonal projection onto the span). */
+#define GSLM_MAX_REST_VIEWS 8
+int gslm_rest_basis(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, float* R_out, void* stream);
+int gslm_rest_coords(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, const float* R, int32_t mode,
+                     const float* in, int64_t in_stride, float* out, int64_t out_stride, void* stream);
 
 /* ---- device-resident CG vector algebra on flat fp32 vectors (param-space, n floats) ----
  * damp_groups: per-element damping is d[group(i)] with group boundaries bounds[0..ngroups]. */

@@ -27,11 +27,12 @@ def main():
         model = model.to("cuda")
         for c in cams:
             c.to("cuda")
-        ref_op = LMProblem(model, cams, torch.zeros(3))
-        ref = _run(ref_op, ref_op.layout)
         op = ShardedLMProblem(model, cams, torch.zeros(3), all_cams=cams, exchange=mode)
         assert op.exchange == mode, (op.exchange, mode)
         got = _run(op, op.layout)
+        # the Gaussian-sharded operator's direction (SH-rest group projected onto the views' span) for both
+        ref_op = LMProblem(model, cams, torch.zeros(3))
+        ref = _run(ref_op, ref_op.layout, v=got.get("v"))
         out["exchanges"][mode] = {
             "loss_rel": abs(float(got["loss"]) - float(ref["loss"])) / float(ref["loss"]),
             "g_max": float((got["g"] - ref["g"]).abs().max() / ref["g"].abs().max()),

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_sizes():
     from gslm import _lib
     lib = _lib.lib
-    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 6
     g1, g2 = lib.gslm_geom_bytes(1000), lib.gslm_geom_bytes(2000)
     assert 0 < g1 < g2
     assert lib.gslm_binning_bytes(10_000, 1080, 1920) > 10_000 * 16
@@ -61,6 +61,18 @@ def test_invalid_arguments_return_error_codes():
         assert lib.gslm_tangent_views(views, n, ctypes.byref(g), ctypes.byref(v), 1, None, 0, None, 0, None,
                                       None) == _lib.GSLM_ERR_INVALID
         assert b"nviews" in lib.gslm_last_error()
+    # SH-rest coordinates (ABI v6): argument checks only (no GPU here)
+    for n in (0, _lib.GSLM_MAX_REST_VIEWS + 1):
+        assert lib.gslm_rest_basis(views, n, ctypes.byref(g), None, None) == _lib.GSLM_ERR_INVALID
+        assert b"nviews" in lib.gslm_last_error()
+    assert lib.gslm_rest_coords(views, 2, ctypes.byref(g), None, 2, None, 0, None, 0, None) == _lib.GSLM_ERR_INVALID
+    assert b"mode" in lib.gslm_last_error()
+    opts = _lib.GslmMatvecOpts()
+    opts.rest_basis, opts.rest_views, opts.view_base = 16, 2, 1
+    g.raw = 1
+    assert lib.gslm_tangent_views(views, 2, ctypes.byref(g), ctypes.byref(v), 1, None, 0, None, 0, ctypes.byref(opts),
+                                  None) == _lib.GSLM_ERR_INVALID
+    assert b"rest_views" in lib.gslm_last_error()
 
 
 def test_dropin_modules_import_with_reference_names():

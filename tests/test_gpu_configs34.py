@@ -126,11 +126,13 @@ def test_config3_slice_multiview_product_and_gaussian_exchange():
     cams_cpu = orbit_cameras(2, W, H, seed=1)
     prob, model, subs, weights = _sampled_problem(1_000_000, cams_cpu, W, H, 10)
     assert not prob.layout.rest_projected
-    v = _direction(prob.layout)
-    y = prob.matvec(v.to(DEV), prob.zeros())
-    # the Gaussian-sharded exchange's pipeline over the same views (one rank: the exchanges are copies)
+    # the Gaussian-sharded exchange's pipeline over the same views (one rank: the exchanges are copies), SH-rest
+    # group in the two views' coordinates: the direction's SH-rest part projected onto their span first
     op = GaussianShardedOperator(prob, all_cams=prob.cams)
     op._exchange_flags()
+    assert op.rest_views == 2
+    v = op.gather_full(op.shard(_direction(prob.layout).to(DEV))).cpu()
+    y = prob.matvec(v.to(DEV), prob.zeros())
     ys = op.gather_full(op.matvec(op.shard(v.to(DEV)), op.zeros()))
     torch.cuda.synchronize()
     y, ys = y.cpu(), ys.cpu()

@@ -1,13 +1,14 @@
 """Per-kernel timeline of the last full forward (k_preprocess .. k_render_fwd) in a rocprofv3 kernel trace:
     python tools/trace_forward.py <run_kernel_trace.csv>"""
 import csv
+import re
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "k_render_fwd" in r["Kernel_Name"]]
 i1 = ends[-1]
-i0 = max(i for i in range(i1) if "k_preprocess<" in rows[i]["Kernel_Name"])
+i0 = max(i for i in range(i1) if re.search(r"k_preprocess(_dma)?<", rows[i]["Kernel_Name"]))
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = None
 busy = 0
