@@ -159,7 +159,9 @@ __device__ __forceinline__ void rest_basis_vec(const ViewK& v, const float* __re
 
 __device__ __forceinline__ double rest_gram(const float A[16], const float B[16], int nc) {
   double acc = 0.0;
-  for (int k = 1; k < nc; ++k) acc += (double)A[k] * (double)B[k];
+#pragma unroll
+  for (int k = 1; k < 16; ++k)
+    if (k < nc) acc += (double)A[k] * (double)B[k];
   return acc;
 }
 
@@ -246,9 +248,11 @@ __global__ __launch_bounds__(256) void k_rest_coords(ViewsK vs, GaussK g, const 
 #pragma unroll
           for (int ch = 0; ch < 3; ++ch) t[k - 1][ch] += (double)B[k] * y[b][ch];
     }
-    for (int k = 1; k < M; ++k)
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) out[i * out_stride + 3 * (k - 1) + ch] = k < nc ? (float)t[k - 1][ch] : 0.f;
+    for (int k = 1; k < 16; ++k)
+      if (k < M)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) out[i * out_stride + 3 * (k - 1) + ch] = k < nc ? (float)t[k - 1][ch] : 0.f;
   } else {
 #pragma unroll
     for (int b = 0; b < MAX_REST_VIEWS; ++b) {
@@ -258,7 +262,9 @@ __global__ __launch_bounds__(256) void k_rest_coords(ViewsK vs, GaussK g, const 
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
         double z = 0.0;
-        for (int k = 1; k < nc && k < M; ++k) z += (double)B[k] * (double)in[i * in_stride + 3 * (k - 1) + ch];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+          if (k < nc && k < M) z += (double)B[k] * (double)in[i * in_stride + 3 * (k - 1) + ch];
 #pragma unroll
         for (int j = 0; j < MAX_REST_VIEWS; ++j)
           if (j < b) z -= Rjb(j, b) * y[j][ch];

@@ -282,12 +282,15 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
       sh_basis_grad(v.D, e.dir[0], e.dir[1], e.dir[2], dB);
       float ddir[3] = {0.f, 0.f, 0.f};
       const int nc = (v.D + 1) * (v.D + 1);
-      for (int k = 1; k < nc; ++k) {
-        const float s0 = g.sh(i, k, 0), s1 = g.sh(i, k, 1), s2 = g.sh(i, k, 2);
-        const float w = dres[0] * s0 + dres[1] * s1 + dres[2] * s2;
+      // compile-time k (unrolled, guarded): dB stays in registers instead of a scratch array indexed at run time
 #pragma unroll
-        for (int j = 0; j < 3; ++j) ddir[j] += dB[k][j] * w;
-      }
+      for (int k = 1; k < 16; ++k)
+        if (k < nc) {
+          const float s0 = g.sh(i, k, 0), s1 = g.sh(i, k, 1), s2 = g.sh(i, k, 2);
+          const float w = dres[0] * s0 + dres[1] * s1 + dres[2] * s2;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) ddir[j] += dB[k][j] * w;
+        }
       const float dd = e.dir[0] * ddir[0] + e.dir[1] * ddir[1] + e.dir[2] * ddir[2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) co.dmean[j] += (ddir[j] - e.dir[j] * dd) / e.dirlen;
@@ -495,11 +498,12 @@ __device__ __forceinline__ void chain_jvp(const ViewK& v, const GaussK& g, const
           for (int ch = 0; ch < 3; ++ch) dres[ch] += nb * t.rest[(i - t.rest_base) * t.rest_stride + ch];
         }
       } else {
-        for (int k = 0; k < nc; ++k) {
-          if (k > 0 && !t.rest) break;
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) dres[ch] += B[k] * t.sh(i, k, ch);
-        }
+        for (int k = 0; k < 16; ++k)
+          if (k < nc && (k == 0 || t.rest)) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) dres[ch] += B[k] * t.sh(i, k, ch);
+          }
       }
     }
     if (t.means3D && v.D > 0) {
@@ -509,11 +513,13 @@ __device__ __forceinline__ void chain_jvp(const ViewK& v, const GaussK& g, const
       for (int j = 0; j < 3; ++j) ddir[j] = (dm[j] - e.dir[j] * dd) / e.dirlen;
       float dB[16][3];
       sh_basis_grad(v.D, e.dir[0], e.dir[1], e.dir[2], dB);
-      for (int k = 1; k < nc; ++k) {
-        const float w = dB[k][0] * ddir[0] + dB[k][1] * ddir[1] + dB[k][2] * ddir[2];
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) dres[ch] += w * g.sh(i, k, ch);
-      }
+      for (int k = 1; k < 16; ++k)
+        if (k < nc) {
+          const float w = dB[k][0] * ddir[0] + dB[k][1] * ddir[1] + dB[k][2] * ddir[2];
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) dres[ch] += w * g.sh(i, k, ch);
+        }
     }
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) T2[6 + ch] = (e.clamped >> ch) & 1u ? 0.f : dres[ch];

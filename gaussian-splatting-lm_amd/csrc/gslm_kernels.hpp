@@ -261,16 +261,14 @@ __device__ __forceinline__ void load_pre_in(const GaussK& g, int64_t i, PreIn& i
   in.x = g.means3D[3 * i + 0];
   in.y = g.means3D[3 * i + 1];
   in.z = g.means3D[3 * i + 2];
-  if (g.cov3D) {
+  // one load per element from a selected address (no branch): with two branches the compiler sank their stores
+  // into one store at a run-time index, which put in.c in scratch memory
+  const bool cv = g.cov3D != nullptr;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) in.c[k] = g.cov3D[6 * i + k];
-  } else {
+  for (int k = 0; k < 3; ++k) in.c[k] = *(cv ? g.cov3D + 6 * i + k : g.scales + 3 * i + k);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) in.c[k] = g.scales[3 * i + k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) in.c[3 + k] = g.rot[4 * i + k];
-    in.qw = g.rot[4 * i + 3];
-  }
+  for (int k = 0; k < 3; ++k) in.c[3 + k] = *(cv ? g.cov3D + 6 * i + 3 + k : g.rot + 4 * i + k);
+  in.qw = cv ? 0.f : g.rot[4 * i + 3];
   in.op = g.opac[i];
 }
 
