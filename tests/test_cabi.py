@@ -139,3 +139,34 @@ def test_product_build_refuses_experiment_flags():
     assert r.returncode != 0 and "not part of the product build" in (r.stdout + r.stderr)
     src = open(os.path.join(csrc, "gslm_device.hpp")).read()
     assert "#error" in src and "GSLM_EXPERIMENT_SKIP_VJP" in src
+
+
+def test_no_product_kernel_uses_scratch(tmp_path):
+    """Every kernel of the shipped gfx950 code object has a zero private segment: no register spills and no
+    local array indexed at run time (which the compiler places in scratch memory, one memory round trip per
+    access).  Read from the code object's AMDGPU metadata notes."""
+    import re
+    import shutil
+    import subprocess
+    from gslm import _lib
+    llvm = "/opt/rocm/lib/llvm/bin"
+    tools = [f"{llvm}/{t}" for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf")]
+    if not all(shutil.which(t) for t in tools):
+        pytest.skip("ROCm LLVM tools not available")
+    fat = tmp_path / "fat.bin"
+    subprocess.run([tools[0], f"--dump-section=.hip_fatbin={fat}", _lib.LIB_PATH, str(tmp_path / "x.so")], check=True)
+    # one offload bundle per translation unit, concatenated
+    blob = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), blob)]
+    notes = ""
+    for k, a in enumerate(starts):
+        part, co = tmp_path / f"b{k}.bin", tmp_path / f"b{k}.co"
+        part.write_bytes(blob[a:starts[k + 1] if k + 1 < len(starts) else len(blob)])
+        subprocess.run([tools[1], "--unbundle", "--type=o", f"--input={part}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        notes += subprocess.run([tools[2], "--notes", str(co)], check=True, capture_output=True, text=True).stdout
+    names = re.findall(r"^\s+\.name:\s+(\S+)", notes, re.M)
+    sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+    assert len(names) == len(sizes) and len(names) > 50
+    assert [n for n, s in zip(names, sizes) if s] == []
