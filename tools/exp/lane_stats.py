@@ -30,7 +30,7 @@ xy, conic, opac = pre["xy"].numpy().astype(np.float32), pre["conic"].numpy().ast
 gx, gy = pre["grid"]
 tiles = range(0, gx * gy, int(sys.argv[1]) if len(sys.argv) > 1 else 41)
 tot = dict(visits=0, lanes=0, valid=0, inv_alpha=0, inv_last=0, inv_outside=0, sub_iters=0, sub_lane_visits=0,
-           pair_iters=0, ent=0, vis_ent=0, half_iters=0, blend_visits=0)
+           pair_iters=0, ent=0, vis_ent=0, half_iters=0, blend_visits=0, fwd_visits=0)
 for t in tiles:
     s, e = int(rg[t, 0]), int(rg[t, 1])
     if e <= s:
@@ -68,6 +68,11 @@ for t in tiles:
         tot["visits"] += nv
         tot["lanes"] += 64 * nv
         tot["blend_visits"] += int(valid[qp].any(axis=0).sum())  # visits some lane of the quadrant blends
+        # the forward blend (no n_contrib yet): hits until every lane has stopped (the stopping entry included),
+        # the whole list when some pixel never reaches T < 1e-4
+        fst = np.where(inside.reshape(-1)[qp], first[qp], -1)
+        fend = fst.max() if (fst < n).all() else n - 1
+        tot["fwd_visits"] += int((reach[qp].any(axis=0) & (np.arange(n) <= fend)).sum())
         v = valid[qp][:, hit]
         tot["valid"] += int(v.sum())
         r = reach[qp][:, hit]
@@ -102,4 +107,5 @@ print(f"visits per wave (quadrant) schedule {tot['visits']}; 4x4 sub-quadrant gr
       f"({tot['sub_iters'] / tot['visits']:.3f}); 16x8 half-tile waves {tot['pair_iters']} x2 px/lane")
 print(f"8x4 half groups (32 lanes) {tot['half_iters']} ({tot['half_iters'] / tot['visits']:.3f})")
 print(f"visits some lane blends {tot['blend_visits']} ({tot['blend_visits'] / tot['visits']:.3f} of the exact-reach schedule)")
+print(f"forward blend visits {tot['fwd_visits']} ({tot['fwd_visits'] / tot['visits']:.3f} of the JVP/VJP schedule)")
 print(f"visited entries / N_dup {tot['vis_ent'] / tot['ent']:.3f}")

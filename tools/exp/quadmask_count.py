@@ -65,7 +65,8 @@ def band(ya, yb):
     return hit, lo, hi
 
 
-old_bits = new_bits = entries = 0
+old_bits = new_bits = entries = exact_bits = 0
+PXO = np.meshgrid(np.arange(8, dtype=f32), np.arange(8, dtype=f32))  # pixel offsets in a quadrant
 H, W = 1080, 1920
 gx_, gy_ = xy[:, 0], xy[:, 1]
 for k in np.nonzero(ok)[0][:20000]:
@@ -91,5 +92,13 @@ for k in np.nonzero(ok)[0][:20000]:
                 hit, lo, hi = band(ya, ya + 7)
                 if hit[0] and xa[0] <= hi[0] and xa[0] + 7 >= lo[0]:
                     new_bits += 1
+                    # exact: some pixel centre of the quadrant with power <= 0 and alpha >= 1/255 (float32)
+                    dx = (gx_[k] - (f32(tx * 16 + 8 * (s & 1)) + PXO[0])).astype(f32)
+                    dy = (gy_[k] - (f32(ty * 16 + 8 * (s >> 1)) + PXO[1])).astype(f32)
+                    pw = f32(-0.5) * (A[k] * dx * dx + C[k] * dy * dy) - B[k] * dx * dy
+                    al = np.minimum(f32(0.99), op[k] * np.exp(pw))
+                    inside = ((f32(tx * 16 + 8 * (s & 1)) + PXO[0]) < W) & ((f32(ty * 16 + 8 * (s >> 1)) + PXO[1]) < H)
+                    if np.any((pw <= 0) & (al >= f32(1 / 255.0)) & inside):
+                        exact_bits += 1
 print(f"entries {entries}: old kept {old_bits} ({old_bits / entries:.3f}/entry), new kept {new_bits} "
-      f"({new_bits / entries:.3f}/entry)")
+      f"({new_bits / entries:.3f}/entry), exact (a pixel centre reached) {exact_bits} ({exact_bits / entries:.3f}/entry)")
