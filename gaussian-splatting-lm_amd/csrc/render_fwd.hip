@@ -37,16 +37,18 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
   tile_pixel(tile_x, tile_y, tid, px, py);
   const bool inside = px < v.W && py < v.H;
   const float pxf = (float)px, pyf = (float)py;
-  bool done = !inside;
   const uint2 range = ranges[tile];
   const int n = (int)(range.y - range.x);
   const uint32_t* pl = point_list + range.x;
   float4* s = s_rec[q];
 
-  float T = 1.0f;
+  // A stopped lane (or one outside the image) carries T = 0, and Tstop its transmittance at the stop: every visit
+  // then runs the same per-lane arithmetic with no boolean lane state across iterations (each one would cost a
+  // few scalar mask instructions per visit; with them the loop was bound by its scalar instructions, not VALU).
+  float T = inside ? 1.0f : 0.0f, Tstop = 0.0f;
   uint32_t last = 0;
   float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  uint64_t dmask = __builtin_amdgcn_ballot_w64(done);  // lanes stopped (or outside the image), wave-uniform
+  uint64_t dmask = __builtin_amdgcn_ballot_w64(!inside);  // lanes stopped (or outside the image), wave-uniform
   for (int base = 0; base < n; base += 64) {
     if (dmask == ~0ull) break;  // every pixel of this quadrant has stopped
     const int k = base + lane;
@@ -71,25 +73,27 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float alpha = fminf(0.99f, b.y * gexp(power));
-      const float test_T = T * (1.0f - alpha);
-      // branch-free visit: a lane that does not blend adds colour * 0 (+-0 leaves every sum unchanged bitwise: they
-      // start at +0 and colours, 1/depth are >= 0) and keeps T; the per-lane state stays in lane masks, no exec juggling
-      const bool live = !done && !(power > 0.0f) && alpha >= 1.0f / 255.0f;
-      const bool stop = live && test_T < 0.0001f;
-      const bool blend = live && !stop;
-      done = done || stop;
-      const float wt = blend ? alpha * T : 0.0f;
+      // u: the alpha the reference blends, 0 where it skips the Gaussian (power > 0, alpha < 1/255): T * (1 - 0)
+      // and colour * 0 leave T and the sums unchanged bitwise (the sums start at +0, colours and 1/depth are >= 0)
+      float u = alpha >= 1.0f / 255.0f ? alpha : 0.0f;
+      u = power > 0.0f ? 0.0f : u;
+      const float test_T = T * (1.0f - u);
+      // a live lane has T >= 1e-4, so with u = 0 it never stops here; a stopped lane (T = 0) re-stops harmlessly
+      const bool stop = test_T < 0.0001f;
+      const float wt = stop ? 0.0f : u * T;
       C0 += b.z * wt;
       C1 += b.w * wt;
       C2 += cc.x * wt;
       if (MODE == FWD_FULL) Dp += cc.y * wt;
-      T = blend ? test_T : T;
-      if (MODE != FWD_LOSS) last = blend ? (uint32_t)(base + j + 1) : last;  // 1-based list position
+      Tstop = stop ? Tstop + T : Tstop;
+      T = stop ? 0.0f : test_T;
+      if (MODE != FWD_LOSS) last = wt > 0.0f ? (uint32_t)(base + j + 1) : last;  // blended: 1-based list position
       dmask |= __builtin_amdgcn_ballot_w64(stop);  // the stop compare's lane mask, no VGPR round trip
       if (dmask == ~0ull) break;
     }
     wave_lds_sync();
   }
+  T = T > 0.0f ? T : Tstop;  // the transmittance the reference keeps: at the stop, else after the last Gaussian
   const int64_t pid = (int64_t)py * v.W + px;
   const int64_t HW = (int64_t)v.H * v.W;
   if constexpr (MODE == FWD_LOSS) {
