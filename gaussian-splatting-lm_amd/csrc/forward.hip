@@ -171,12 +171,11 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   __syncthreads();
   const uint32_t total = s_off[256];
   for (uint32_t e = tid; e < total; e += 256) {
-    int lo = 0, hi = 255;  // last t with s_off[t] <= e (s_off[0] = 0)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= e) lo = mid;
-      else hi = mid - 1;
-    }
+    // last t with s_off[t] <= e (s_off[0] = 0; non-decreasing, 0xFFFFFFFF past the block's last Gaussian): 8 fixed
+    // steps, no divergent loop (its per-lane exit made every step a few scalar exec-mask instructions)
+    int lo = 0;
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1) lo = s_off[lo + step] <= e ? lo + step : lo;
     const uint32_t li = e - s_off[lo];
     const uint32_t w = s_rc[lo][2];
     const uint32_t dy = li / w;
