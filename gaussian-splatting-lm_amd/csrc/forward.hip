@@ -57,7 +57,11 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* _
   rec[RECS * i + 1] = r1;
   rec[RECS * i + 2] = r2;
   tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
-  rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  const uint2 rc = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  rect[i] = rc;
+  // the rect again in the record's padding slot: k_duplicate's random per-Gaussian read is then one 64-B record
+  // (one cache line) instead of the record and a rect line
+  rec[RECS * i + 3] = make_float4(__uint_as_float(rc.x), __uint_as_float(rc.y), 0.f, 0.f);
   clampw[i] = o.clamped;  // read only where tiles[i] != 0
   if (radii_out) radii_out[i] = o.radius;
 }
@@ -125,7 +129,11 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
   rec[RECS * i + 1] = r1;
   rec[RECS * i + 2] = r2;
   tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
-  rect[i] = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  const uint2 rc = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+  rect[i] = rc;
+  // the rect again in the record's padding slot: k_duplicate's random per-Gaussian read is then one 64-B record
+  // (one cache line) instead of the record and a rect line
+  rec[RECS * i + 3] = make_float4(__uint_as_float(rc.x), __uint_as_float(rc.y), 0.f, 0.f);
   clampw[i] = o.clamped;
   if (radii_out) radii_out[i] = o.radius;
 }
@@ -155,7 +163,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
     n = (s + 1 < P ? offsets[s + 1] : N) - o;
     s_off[tid] = o - base;
     if (n) {
-      const uint2 rc = rect[g];
+      const float4 r3 = rec[RECS * (int64_t)g + 3];  // the rect (k_preprocess' copy in the record's padding)
+      const uint2 rc = make_uint2(__float_as_uint(r3.x), __float_as_uint(r3.y));
       const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
       s_rc[tid][0] = (uint32_t)x0;
       s_rc[tid][1] = (uint32_t)y0;
