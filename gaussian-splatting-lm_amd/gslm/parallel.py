@@ -83,8 +83,13 @@ def _staged(fn, *tensors):
 
 class ShardedOperator:
     SCREEN_FLOATS = 8  # per (view, Gaussian) in the screen exchange
-    supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
     supports_cg_ctl = True  # cgls_fused's device control block, passed to the local products
+
+    @property
+    def supports_exposure_zero(self):
+        """Without collectives (one rank) the products are the local problem's, its exposure-slice skip included;
+        the exchanges' products write y themselves."""
+        return (not collectives_on(self.world_size)) and getattr(self.local, "supports_exposure_zero", False)
 
     def __init__(self, local, group=None, all_cams=None, exchange="auto"):
         self.local = local
@@ -133,11 +138,13 @@ class ShardedOperator:
         self.local.rhs(out)
         return self._allreduce(out)
 
-    def matvec_dot(self, v, y, dot_out, pre=None, cg_ctl=None):
+    def matvec_dot(self, v, y, dot_out, pre=None, cg_ctl=None, exposure_zero=False):
         kw = {} if pre is None else {"pre": pre}
         if cg_ctl is not None:
             kw["cg_ctl"] = cg_ctl
         if not collectives_on(self.world_size):
+            if exposure_zero:
+                kw["exposure_zero"] = True
             return self.local.matvec_dot(v, y, dot_out, **kw)
         if self.exchange == "screen":
             return self._matvec_screen(v, y, dot_out, pre, cg_ctl)
