@@ -759,7 +759,7 @@ class LossEvaluator:
     Each view's loss lands in its own device double; the total is their sum (view order fixed, so run to run the
     same).  `reduce`: a callable summing it over the ranks that hold the other views (gslm.parallel.allreduce_loss)."""
 
-    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None, streams=4):
+    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None, streams=8):
         self.model = model
         self.device = device
         self.reduce = reduce

@@ -15,6 +15,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--views", type=int, default=50)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--P", type=int, default=1_000_000)
+ap.add_argument("--streams", type=int, nargs="*", default=[1, 2, 3, 4])
+ap.add_argument("--batch", type=int, default=8)
 a = ap.parse_args()
 from gslm.cameras import orbit_cameras  # noqa: E402
 from gslm.lm import LossEvaluator  # noqa: E402
@@ -26,10 +28,10 @@ cams = orbit_cameras(a.views, 1920, 1080, seed=5)
 for c in cams:
     c.to(dev)
     c.original_image = torch.rand(3, 1080, 1920, device=dev)
-out = {"views": a.views, "P": a.P}
+out = {"views": a.views, "P": a.P, "batch": a.batch}
 ref = None
-for ns in (1, 2, 3, 4):
-    ev = LossEvaluator(model, cams, torch.zeros(3), device=dev, streams=ns)
+for ns in a.streams:
+    ev = LossEvaluator(model, cams, torch.zeros(3), device=dev, streams=ns, batch=max(a.batch, ns))
     v = float(ev.evaluate())  # sorts the depth orders
     ref = v if ref is None else ref
     for _ in range(2):
