@@ -250,14 +250,30 @@ def main():
     if getattr(prob, "exchange", None) == "gaussian" and hasattr(prob, "stage_times"):
         shard_stages = prob.stage_times(g, reps=max(args.steps, 5))
 
-    # ---------------- raster Mpix/s: full forwards (preprocess, sort, binning, blend; includes the
-    # num_rendered read-back the upstream forward also does)
+    # ---------------- raster Mpix/s: full forwards (preprocess, depth sort, binning, tile sort, ranges, blend) through
+    # the device-count form (gslm_rasterize_dev: the pair count stays on the device, no host round trip between the
+    # preprocess and the binning); each render's count is checked against its list capacity after the timed loop.
+    # `raster_sync_mpix_s`: the same forwards with the count read back per view (gslm_forward's protocol, as upstream)
     fsteps = args.forward_steps or args.steps
     from gslm.params import raw_gaussians
     graw = raw_gaussians(model)
     for vr in prob.views:
         vr.forward(graw, prob.stream)
+    counts = torch.zeros(max(fsteps, 1) * len(prob.views), dtype=torch.int32, device=device)
+    caps = [vr.capacity() for vr in prob.views]
     barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(fsteps):
+        for j, vr in enumerate(prob.views):
+            vr.forward_dev(graw, prob.stream, n_out=counts.data_ptr() + 4 * (it * len(prob.views) + j))
+    torch.cuda.synchronize()
+    barrier()
+    t_fwd = max_over_ranks(time.perf_counter() - t0)
+    cnt = counts.view(max(fsteps, 1), len(prob.views)).tolist()
+    if any(c[j] > caps[j] for c in cnt[:fsteps] for j in range(len(caps))):
+        raise RuntimeError(f"raster timing: a pair count exceeded its list capacity ({cnt[0]} vs {caps})")
+    mpix = n_views * W * H * fsteps / t_fwd / 1e6
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(fsteps):
@@ -265,8 +281,8 @@ def main():
             vr.forward(graw, prob.stream)
     torch.cuda.synchronize()
     barrier()
-    t_fwd = max_over_ranks(time.perf_counter() - t0)
-    mpix = n_views * W * H * fsteps / t_fwd / 1e6
+    t_fwd_sync = max_over_ranks(time.perf_counter() - t0)  # (leaves every view in forward()'s exact layout)
+    mpix_sync = n_views * W * H * fsteps / t_fwd_sync / 1e6
 
     # ---------------- roofline of the dominant kernel: the fused JVP->VJP tile pass (k_render_matvec)
     loc = getattr(prob, "local", prob)  # the rank's own LMProblem (full P) under a sharded operator
@@ -279,21 +295,23 @@ def main():
     def stage(mask):
         opts = _lib.GslmMatvecOpts()
         opts.stages = mask | (8 if mask == 4 else 0)  # the gather in its CG form: overwrite + D v
-        opts.flags = (1 if mask == 2 else 0) | loc.mv_flags  # GSLM_MV_TAIL_CLEAN: as inside the CG loop
+        opts.flags = 1 | loc.mv_flags  # GSLM_MV_TAIL_CLEAN: the geometry's derived state built (opts0), as in the CG loop
         opts.damp7 = loc._damps if mask == 4 else None
         check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs),
                                       loc.weights[0].data_ptr(), 1, vr.geom.data_ptr(), vr.binning.data_ptr(),
                                       vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
                                       ctypes.byref(ys), ctypes.byref(opts), loc.stream))
 
-    stage(1)
     opts0 = _lib.GslmMatvecOpts()
-    opts0.stages = 2  # RENDER once with the tail rows written: the state every CG iteration after the first sees
+    # RENDER once without GSLM_MV_TAIL_CLEAN (the forwards above rewrote the binning): the row map and, with the
+    # projected LM rows, the linearisation record rebuilt -- the state every CG iteration after the first sees
+    opts0.stages = 2
     opts0.flags = loc.mv_flags
     check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(graw), ctypes.byref(vs), loc.weights[0].data_ptr(),
                                   1, vr.geom.data_ptr(), vr.binning.data_ptr(), vr.N, vr.image.data_ptr(),
                                   vr.scratch.data_ptr(), vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(opts0),
                                   loc.stream))
+    stage(1)
     stage(2)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = max(args.steps, 5)
@@ -344,7 +362,8 @@ def main():
     raster_roofline = {"bound": "hbm", "achieved": b_fwd / fwd_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": b_fwd / fwd_s / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_view": b_fwd,
                        "model": "SURVEY 8(d) B_fwd = 4F P + 48 P + 88 N_dup + 24 HW, over the full forward "
-                                "(preprocess, depth sort, binning, tile sort, ranges, blend, num_rendered read-back)"}
+                                "(preprocess, depth sort, binning, tile sort, ranges, blend; the pair count on the "
+                                "device, gslm_rasterize_dev)"}
 
     # the side measurements below run on one view and need the memory of the batch's problem back
     # (at configs[4], 5M Gaussians x 32 4K views, that is ~100 GB)
@@ -424,6 +443,9 @@ def main():
                                               "at their steady state, as in a running LM solve"),
             "raster_mpix_s": mpix,
             "forward_ms_per_view": 1e3 * t_fwd / fsteps / max(n_views_local, 1),
+            "raster_sync": {"mpix_s": mpix_sync, "forward_ms_per_view": 1e3 * t_fwd_sync / fsteps / max(n_views_local, 1),
+                            "note": "the same forwards with the pair count read back by the host before the binning "
+                                    "(gslm_forward's protocol, as the upstream forward)"},
             "num_rendered": n_rendered,
             "stage_ms": {"tangent_preprocess": tangent_ms, "render_matvec": render_ms, "gather_backward": gather_ms},
             "roofline": {"bound": "hbm", "kernel": "k_render_matvec", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -290,6 +290,70 @@ int gslm_rasterize_loss(const gslm_view* view, int64_t P, void* geom, void* binn
   return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0, s);
 }
 
+// ---- device-count forms: the pair count stays on the device (no read-back between preprocess and binning) ----
+int64_t gslm_binning_capacity(size_t binning_bytes, int32_t H, int32_t W) {
+  if (H <= 0 || W <= 0 || binning_bytes < gslm_binning_bytes(0, H, W)) return 0;
+  // gslm_binning_bytes is non-decreasing in N: the largest N that fits, by bisection
+  int64_t lo = 0, hi = (int64_t)1 << 40;
+  while (hi - lo > 1) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (gslm_binning_bytes(mid, H, W) <= binning_bytes) lo = mid;
+    else hi = mid;
+  }
+  return lo > (int64_t)0xFFFFFFFFu ? (int64_t)0xFFFFFFFFu : lo;
+}
+
+int gslm_rasterize_dev(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes, void* image,
+                       size_t image_bytes, float* out_color, float* out_invdepth, uint32_t* n_out, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (image_bytes < gslm_image_bytes(v.H, v.W)) { set_error("image workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (!out_color) { set_error("out_color is NULL"); return GSLM_ERR_INVALID; }
+  const int64_t cap = gslm_binning_capacity(binning_bytes, v.H, v.W);
+  if (binning_bytes < gslm_binning_bytes(0, v.H, v.W)) { set_error("binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  GeomBufs gb;
+  BinBufs bb;
+  ImgBufs ib;
+  geom_layout(P, geom, &gb);
+  bin_layout(cap, v.gx * v.gy, binning, &bb);
+  img_layout(v.H, v.W, image, &ib);
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = launch_binning(v, P, gb, bb, cap, s, true, n_out))) return st;
+  return launch_render_fwd(v, gb, bb, ib, out_color, out_invdepth, s);
+}
+
+int gslm_rasterize_loss_dev(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                            const float* gt, const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
+                            int32_t accumulate, uint32_t* n_out, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (binning_bytes < gslm_binning_bytes(0, v.H, v.W)) { set_error("binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (scratch_bytes < gslm_loss_scratch_bytes(v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
+  if (!gt || !loss_dev || !scratch) { set_error("rasterize_loss: NULL gt / loss / scratch"); return GSLM_ERR_INVALID; }
+  const int64_t cap = gslm_binning_capacity(binning_bytes, v.H, v.W);
+  GeomBufs gb;
+  BinBufs bb;
+  geom_layout(P, geom, &gb);
+  bin_layout(cap, v.gx * v.gy, binning, &bb);
+  hipStream_t s = (hipStream_t)stream;
+  if ((st = launch_binning(v, P, gb, bb, cap, s, true, n_out))) return st;
+  return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0, s);
+}
+
+int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream) {
+  if (!dst || (P > 0 && !geom)) { set_error("num_rendered_copy: NULL geom / dst"); return GSLM_ERR_INVALID; }
+  if (P == 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(dst, 0, 4, (hipStream_t)stream));
+    return GSLM_OK;
+  }
+  GeomBufs gb;
+  geom_layout(P, const_cast<void*>(geom), &gb);
+  GSLM_HIP_CHECK(hipMemcpyAsync(dst, gb.counters, 4, hipMemcpyDefault, (hipStream_t)stream));
+  return GSLM_OK;
+}
+
 int gslm_forward(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, void* binning,
                  size_t binning_bytes, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
                  int32_t* out_radii, int64_t* out_num_rendered, void* stream) {

@@ -142,8 +142,12 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
 // output range, written by the whole block in element order (coalesced, and a large Gaussian's tiles are
 // spread over the block instead of one thread's loop).  Element e belongs to the last Gaussian whose
 // local offset is <= e (binary search in LDS); inside a Gaussian the rect is walked row-major.
+// n_dev (or NULL): N is the list capacity and *n_dev the pair count (the depth-order scan's total, not read back
+// by the host: gslm_rasterize_dev); pairs past the capacity are not written (the host sees the count and renders
+// that view again with a larger list)
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                     const uint32_t* __restrict__ offsets, uint32_t N,
+                                                    const uint32_t* __restrict__ n_dev,
                                                     const uint2* __restrict__ rect, const float4* __restrict__ rec,
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   __shared__ QuadCull s_q[256];
@@ -154,13 +158,14 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
   const int64_t slast = min(s0 + 255, P - 1);
   const uint32_t base = offsets[s0];
+  const uint32_t Ntot = n_dev ? *n_dev : N;
   uint32_t n = 0;
   if (s < P) {
     const uint32_t g = sorted_idx[s];
     // the tile count from the depth-order scan (coalesced) instead of tiles[g] (a random line per Gaussian);
     // culled Gaussians (n = 0) then touch nothing else
     const uint32_t o = offsets[s];
-    n = (s + 1 < P ? offsets[s + 1] : N) - o;
+    n = (s + 1 < P ? offsets[s + 1] : Ntot) - o;
     s_off[tid] = o - base;
     if (n) {
       const float4 r3 = rec[RECS * (int64_t)g + 3];  // the rect (k_preprocess' copy in the record's padding)
@@ -178,7 +183,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
   }
   if (s == slast) s_off[256] = offsets[s] - base + n;
   __syncthreads();
-  const uint32_t total = s_off[256];
+  // the block's pairs [base, base + total), clipped to the capacity (a no-op when N is the count)
+  const uint32_t total = base < N ? min(s_off[256], N - base) : 0u;
   for (uint32_t e = tid; e < total; e += 256) {
     // last t with s_off[t] <= e (s_off[0] = 0; non-decreasing, 0xFFFFFFFF past the block's last Gaussian): 8 fixed
     // steps, no divergent loop (its per-lane exit made every step a few scalar exec-mask instructions)
@@ -230,9 +236,16 @@ __global__ __launch_bounds__(256) void k_point_ids(int64_t N, const uint32_t* __
   if (k < N) out[k] = pl_id(pl[k]);
 }
 
+// n_dev (or NULL): as k_duplicate (N the capacity, *n_dev the count); n_out (or NULL) receives the count
 __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __restrict__ keys,
-                                                 uint2* __restrict__ ranges) {
+                                                 uint2* __restrict__ ranges, const uint32_t* __restrict__ n_dev,
+                                                 uint32_t* __restrict__ n_out) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n_dev) {
+    const uint32_t c = *n_dev;
+    if (n_out && k == 0) *n_out = c;
+    N = min(N, (int64_t)c);
+  }
   if (k >= N) return;
   const uint32_t t = keys[k];
   if (k == 0 || keys[k - 1] != t) ranges[t].x = (uint32_t)k;
@@ -335,27 +348,35 @@ int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* 
   return GSLM_OK;
 }
 
-int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s) {
+int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s,
+                   bool device_count, uint32_t* n_out) {
   const int ntiles = v.gx * v.gy;
+  // device_count: N is the list capacity, the pair count stays on the device (gb.counters[0])
+  const uint32_t* n_dev = device_count ? gb.counters : nullptr;
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0)
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
-                       gb.offsets, (uint32_t)N, gb.rect, gb.rec, bb.keys0, bb.vals0);
+                       gb.offsets, (uint32_t)N, n_dev, gb.rect, gb.rec, bb.keys0, bb.vals0);
   GSLM_LAUNCH_CHECK();
   if (N == 0) {  // every range stays [0, 0); the tile passes still read a launch order
+    if (n_out) {
+      if (P > 0) GSLM_HIP_CHECK(hipMemcpyAsync(n_out, gb.counters, 4, hipMemcpyDeviceToDevice, s));
+      else GSLM_HIP_CHECK(hipMemsetAsync(n_out, 0, 4, s));
+    }
     hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
     GSLM_LAUNCH_CHECK();
     return GSLM_OK;
   }
   bool alt = false;
-  int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s);
+  int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s, false, nullptr,
+                            n_dev);
   if (st != GSLM_OK) return st;
   if ((alt ? bb.vals1 : bb.vals0) != bb.point_list) {
     set_error("internal: radix pass count disagrees with the binning layout");
     return GSLM_ERR_INVALID;
   }
   const unsigned nbN = (unsigned)((N + 255) / 256);
-  hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges);
+  hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, n_dev, n_out);
   GSLM_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
   GSLM_LAUNCH_CHECK();

@@ -57,9 +57,10 @@ inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_b
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
 // ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
 // last_gather (or NULL): the last pass writes last_gather[value] in place of each sorted key.
+// n_dev (or NULL): n is a capacity (grid and hist sized for it) and the kernels sort the first min(n, *n_dev) pairs.
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
                      uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false,
-                     const uint32_t* last_gather = nullptr);
+                     const uint32_t* last_gather = nullptr, const uint32_t* n_dev = nullptr);
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;

@@ -436,7 +436,10 @@ size_t img_layout(int H, int W, void* base, ImgBufs* out);
 size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
 
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
-int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s);
+// device_count: N is the list capacity and the count stays on the device (gslm_rasterize_dev); n_out (device, or
+// NULL) receives the count
+int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s,
+                   bool device_count = false, uint32_t* n_out = nullptr);
 int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,
                      int64_t N, hipStream_t s);
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);

@@ -49,12 +49,15 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
   return inc + off;
 }
 
+// n_dev (or NULL): the key count is min(n, *n_dev), read on the device (a capacity-sized launch whose count the host
+// has not read back: gslm_rasterize_dev); blocks past it count nothing
 template <int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n,
                                                              int shift, uint32_t dmask, uint32_t* __restrict__ hist,
-                                                             int nblocks) {
+                                                             int nblocks, const uint32_t* __restrict__ n_dev) {
   __shared__ uint32_t cnt[RADIX];
   const int tid = threadIdx.x;
+  if (n_dev) n = min(n, (int64_t)*n_dev);
   cnt[tid] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * (SORT_THREADS * ITEMS);
@@ -96,7 +99,7 @@ template <int ITEMS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
-    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather) {
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather, const uint32_t* __restrict__ n_dev) {
   static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
   constexpr int TILE = SORT_THREADS * ITEMS;
   constexpr int WAVE_KEYS = TILE / 4;
@@ -106,8 +109,9 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   __shared__ uint32_t s_gbase[RADIX];    // global offset of this block's run of each digit
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (n_dev) n = min(n, (int64_t)*n_dev);  // as k_radix_hist; a block past the count moves nothing (nvalid <= 0)
   const int64_t base = (int64_t)blockIdx.x * TILE;
-  const int nvalid = (int)min<int64_t>(TILE, n - base);
+  const int nvalid = (int)max<int64_t>(-1, min<int64_t>(TILE, n - base));
   const int wbase = w * WAVE_KEYS;
   const uint32_t dmask = (1u << nbits) - 1u;
 
@@ -371,7 +375,8 @@ int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* o
 }
 
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
-                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values, const uint32_t* last_gather) {
+                     uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values, const uint32_t* last_gather,
+                     const uint32_t* n_dev) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const int nb = (int)sort_blocks(n);
@@ -390,15 +395,16 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
     const uint32_t* vin = (first && iota_values) ? (const uint32_t*)nullptr : vi;
     const uint32_t* kg = (shift + per >= end_bit) ? last_gather : nullptr;  // the last pass
     if (small) {
-      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
+      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb,
+                         n_dev);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
       hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift,
-                         nbits, hist, nb, totals, kg);
+                         nbits, hist, nb, totals, kg, n_dev);
     } else {
-      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb);
+      hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb, n_dev);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
       hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift, nbits,
-                         hist, nb, totals, kg);
+                         hist, nb, totals, kg, n_dev);
     }
     first = false;
     GSLM_LAUNCH_CHECK();

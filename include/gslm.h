@@ -20,9 +20,9 @@
  * Conventions: raw device pointers, sizes, a settings POD and a hipStream_t (passed as void*).
  * Every function returns GSLM_OK (0) or a negative status; gslm_last_error() describes the last
  * failure.  No internal threads, no allocation (the caller allocates workspaces sized by the
- * *_bytes queries), stream ordered, not re-entrant on one workspace.  Only gslm_num_rendered and
+ * *_bytes queries), stream ordered, not re-entrant on one workspace.  Only gslm_num_rendered(_many) and
  * gslm_forward (which calls it) synchronise the stream (the upstream forward does the same to
- * size its binning buffers).
+ * size its binning buffers); the *_dev rasterize forms do not.
  */
 #ifndef GSLM_H
 #define GSLM_H
@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 6
+#define GSLM_ABI_VERSION 7
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -140,6 +140,22 @@ size_t gslm_loss_scratch_bytes(int32_t H, int32_t W);
 int gslm_rasterize_loss(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
                         int64_t num_rendered, const float* gt, const float* alpha_mask, void* scratch,
                         size_t scratch_bytes, double* loss_dev, int32_t accumulate, void* stream);
+/* Device-count forms (ABI 7): no host read-back of the pair count between gslm_preprocess and the binning.  The
+ * binning workspace is used as a list of gslm_binning_capacity(binning_bytes, H, W) pairs; the count stays in the
+ * geometry workspace and the kernels read it there.  n_out (device or host-pinned uint32, nullable) receives the count
+ * in stream order: when it exceeds the capacity the pairs past it were dropped and the image / loss is invalid -- render
+ * the view again with gslm_rasterize and a buffer of gslm_binning_bytes(count).  The binning written here serves this
+ * render only (gslm_backward / gslm_jvp / gslm_matvec_* take the layout of the exact count: use gslm_rasterize for
+ * those).  Same pairs, order, image and loss as gslm_rasterize / gslm_rasterize_loss whenever the count fits. */
+int64_t gslm_binning_capacity(size_t binning_bytes, int32_t H, int32_t W);
+int gslm_rasterize_dev(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                       void* image, size_t image_bytes, float* out_color, float* out_invdepth, uint32_t* n_out,
+                       void* stream);
+int gslm_rasterize_loss_dev(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
+                            const float* gt, const float* alpha_mask, void* scratch, size_t scratch_bytes,
+                            double* loss_dev, int32_t accumulate, uint32_t* n_out, void* stream);
+/* Stream-ordered 4-byte copy of gslm_preprocess' pair count to dst (device or host-pinned); no synchronisation. */
+int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream);
 /* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
  * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
  * gslm_rasterize with a larger buffer). */

@@ -28,12 +28,28 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_sizes():
     from gslm import _lib
     lib = _lib.lib
-    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 7
     g1, g2 = lib.gslm_geom_bytes(1000), lib.gslm_geom_bytes(2000)
     assert 0 < g1 < g2
     assert lib.gslm_binning_bytes(10_000, 1080, 1920) > 10_000 * 16
     assert lib.gslm_image_bytes(1080, 1920) >= 1080 * 1920 * 8
     assert lib.gslm_scratch_bytes(1000, 5000) >= 1000 * 48 + 5000 * 48
+
+
+def test_binning_capacity_is_the_largest_fitting_list():
+    """gslm_binning_capacity (ABI 7, the device-count rasterize forms): the largest pair count whose binning layout fits
+    the workspace -- host arithmetic only."""
+    from gslm import _lib
+    lib = _lib.lib
+    for H, W in ((1080, 1920), (40, 56), (2160, 3840)):
+        for n in (0, 1, 4095, 4096, 4_867_236, 6_000_000):
+            b = lib.gslm_binning_bytes(n, H, W)
+            for extra in (0, 3, 4096):
+                cap = lib.gslm_binning_capacity(b + extra, H, W)
+                assert cap >= n
+                assert lib.gslm_binning_bytes(cap, H, W) <= b + extra < lib.gslm_binning_bytes(cap + 1, H, W)
+        assert lib.gslm_binning_capacity(lib.gslm_binning_bytes(0, H, W) - 1, H, W) == 0
+    assert lib.gslm_num_rendered_copy(None, 5, None, None) == _lib.GSLM_ERR_INVALID
 
 
 def test_invalid_arguments_return_error_codes():

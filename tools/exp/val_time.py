@@ -17,6 +17,7 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--P", type=int, default=1_000_000)
 ap.add_argument("--streams", type=int, nargs="*", default=[1, 2, 3, 4])
 ap.add_argument("--batch", type=int, default=8)
+ap.add_argument("--readback", action="store_true", help="also time the per-batch count read-back path (device_count=False)")
 a = ap.parse_args()
 from gslm.cameras import orbit_cameras  # noqa: E402
 from gslm.lm import LossEvaluator  # noqa: E402
@@ -30,8 +31,9 @@ for c in cams:
     c.original_image = torch.rand(3, 1080, 1920, device=dev)
 out = {"views": a.views, "P": a.P, "batch": a.batch}
 ref = None
-for ns in a.streams:
-    ev = LossEvaluator(model, cams, torch.zeros(3), device=dev, streams=ns, batch=max(a.batch, ns))
+runs = [(ns, True) for ns in a.streams] + ([(ns, False) for ns in a.streams] if a.readback else [])
+for ns, dc in runs:
+    ev = LossEvaluator(model, cams, torch.zeros(3), device=dev, streams=ns, batch=max(a.batch, ns), device_count=dc)
     v = float(ev.evaluate())  # sorts the depth orders
     ref = v if ref is None else ref
     for _ in range(2):
@@ -41,7 +43,8 @@ for ns in a.streams:
     for _ in range(a.reps):
         ev.evaluate()
     torch.cuda.synchronize()
-    out[f"streams{ns}_ms_per_view"] = 1e3 * (time.perf_counter() - t0) / a.reps / a.views
-    out[f"streams{ns}_rel_diff"] = abs(v - ref) / abs(ref)
+    tag = f"streams{ns}" + ("" if dc else "_readback")
+    out[f"{tag}_ms_per_view"] = 1e3 * (time.perf_counter() - t0) / a.reps / a.views
+    out[f"{tag}_rel_diff"] = abs(v - ref) / abs(ref)
     del ev
 print(json.dumps(out), flush=True)
