@@ -342,10 +342,14 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         t[q] = 0.f;
         if (q_used<WITH_XY, WITH_INV>(q)) {
           const int sq = q_slot<WITH_XY, WITH_INV>(q);
-          const float p0 = (my_mask & 1u) ? s_acc[(0 * NU + sq) * ACC_STRIDE + tid] : 0.f;
-          const float p1 = (my_mask & 2u) ? s_acc[(1 * NU + sq) * ACC_STRIDE + tid] : 0.f;
-          const float p2 = (my_mask & 4u) ? s_acc[(2 * NU + sq) * ACC_STRIDE + tid] : 0.f;
-          const float p3 = (my_mask & 8u) ? s_acc[(3 * NU + sq) * ACC_STRIDE + tid] : 0.f;
+          // every wave's slot read, the ones it never wrote (no hit) then dropped by a select: plain LDS loads and
+          // v_cndmask instead of an exec-mask branch around each load
+          const float a0 = s_acc[(0 * NU + sq) * ACC_STRIDE + tid], a1 = s_acc[(1 * NU + sq) * ACC_STRIDE + tid];
+          const float a2 = s_acc[(2 * NU + sq) * ACC_STRIDE + tid], a3 = s_acc[(3 * NU + sq) * ACC_STRIDE + tid];
+          const float p0 = (my_mask & 1u) ? a0 : 0.f;
+          const float p1 = (my_mask & 2u) ? a1 : 0.f;
+          const float p2 = (my_mask & 4u) ? a2 : 0.f;
+          const float p3 = (my_mask & 8u) ? a3 : 0.f;
           t[q] = ((p0 + p1) + p2) + p3;
         }
       }
