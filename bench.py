@@ -373,13 +373,16 @@ def main():
     del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
 
-    fb = c0_gpu = lm = lm_tv = ssim = fo = dropin = None
+    fb = c0_gpu = lm = lm_tv = lm_ref = ssim = fo = dropin = None
     if not args.no_side:
         # ---------------- BASELINE configs[2] / [3] as train_jvp.py runs it, on every rank: one full LM step (loss,
         # J^T b, CGLS with 10 iterations and the reference's stopping tests, the 7-point line search on the
         # reference's 50 validation views), sharded over the ranks; and with the training batch as the validation set
         lm = time_lm_step(model, cams_all, val_all, bg)
         lm_tv = time_lm_step(model, cams_all, cams_all, bg, reps=1, with_timing=False)
+        # the reference's own CGLS schedule, max_iter = 2, restart_iter = 1 (train_jvp.py:254-256; SURVEY 8(d) config 3
+        # "the reference-schedule (2 x 1) variant is also reported")
+        lm_ref = time_lm_step(model, cams_all, val_all, bg, iters=2, restart=1, reps=1)
         # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
         # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
         fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
@@ -464,6 +467,7 @@ def main():
             "sharded_stage_ms": shard_stages,
             "lm_step": lm,
             "lm_step_val_is_train": lm_tv,
+            "lm_step_ref_schedule": lm_ref,
             "ssim_cg": ssim,
             "first_order": fo,
             "cg_full_layout": cg_full,
@@ -612,8 +616,9 @@ def time_ssim_cg(model, cams, bg, steps=10):
             "ms_per_step": 1e3 * t, "view_matvec_per_s": len(cams) / t}
 
 
-def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True):
-    """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = restart_iter = iters and the reference's stopping
+def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True, restart=None):
+    """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = iters, restart_iter = restart (default iters) and the
+    reference's stopping
     tests (on the device), the line search over `val_cams`; every rank calls it (the training and validation views
     are sharded over the ranks inside).  The model is restored after each step, so every rep solves the same
     problem; the phase breakdown (evaluate + J^T b, CG, line search) comes from one more step with timing=True."""
@@ -625,14 +630,15 @@ def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True):
             for t, s0 in zip(model.params(), saved):
                 t.copy_(s0)
 
-    out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters)  # warm-up (workspaces, clocks)
+    restart = iters if restart is None else restart
+    out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart)  # warm-up (workspaces, clocks)
     restore()
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters)
+        out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart)
         restore()
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
@@ -640,14 +646,15 @@ def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True):
         tt = torch.tensor([t], dtype=torch.float64, device=saved[0].device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    res = {"config": f"full LM step, {len(cams)} training view(s) over {out['ranks']} rank(s), CGLS {iters} iterations "
+    sched = f"{iters} iterations" if restart == iters else f"max_iter {iters} x restart_iter {restart} (the reference's schedule)"
+    res = {"config": f"full LM step, {len(cams)} training view(s) over {out['ranks']} rank(s), CGLS {sched} "
                      f"with the reference's stopping tests + 7-point line search on {len(val_cams)} validation "
                      "view(s) (train_jvp.py:237-279; BASELINE configs[2], configs[3] at 8 GPUs)",
            "ms": 1e3 * t, "cg_iters": out["cg"]["iters"], "val_views": len(val_cams), "ranks": out["ranks"],
            "val_renders_per_rank": 7 * -(-len(val_cams) // out["ranks"]),
            "loss_start": out["start_loss"], "loss_final": out["final_val_loss"], "best_alpha": out["best_alpha"]}
     if with_timing:
-        o2 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=iters, timing=True)
+        o2 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart, timing=True)
         restore()
         res["breakdown_ms"] = o2["timing"]
     return res
