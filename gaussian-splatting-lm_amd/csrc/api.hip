@@ -54,7 +54,7 @@ size_t bin_layout(int64_t N, int ntiles, void* base, BinBufs* o) {
   b.hist = c.take<uint32_t>(sort_hist_bytes(N) / 4);
   b.ranges = c.take<uint2>(ntiles);
   b.tile_order = c.take<uint32_t>(ntiles);
-  b.tile_neff = c.take<uint32_t>(ntiles);
+  b.tile_neff = c.take<uint32_t>((size_t)4 * ntiles);
   b.end_bit = 1;
   while ((1ll << b.end_bit) < (long long)ntiles) ++b.end_bit;
   b.passes = (b.end_bit + 7) / 8;

@@ -255,19 +255,25 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __res
 // ---- the LM row map (ScratchBufs::hscan), once per geometry ----
 // Computed by the first LM product on a geometry (GSLM_MV_TAIL_CLEAN protocol), not by the forward: the
 // goff / rect gathers are random over 12 B per Gaussian and the drop-in backward does not need the map.
-// largest n_contrib over each tile's pixels: list positions at or past it are blended by no pixel of the tile
+// largest n_contrib over each tile quadrant's pixels (wave q's 8x8 block, tile_pixel): list positions at or past it
+// are blended by no pixel of that quadrant
 __global__ __launch_bounds__(256) void k_tile_neff(ViewK v, const uint32_t* __restrict__ n_contrib,
                                                     uint32_t* __restrict__ neff) {
-  __shared__ int s_w[4];
   const int tile = blockIdx.x, tile_x = tile % v.gx, tile_y = tile / v.gx;
   int px, py;
   tile_pixel(tile_x, tile_y, threadIdx.x, px, py);
   int wm = (px < v.W && py < v.H) ? (int)n_contrib[(int64_t)py * v.W + px] : 0;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) wm = max(wm, __shfl_xor(wm, o));
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = wm;
-  __syncthreads();
-  if (threadIdx.x == 0) neff[tile] = (uint32_t)max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+  if ((threadIdx.x & 63) == 0) neff[4 * tile + (threadIdx.x >> 6)] = (uint32_t)wm;
+}
+
+// The quadrants whose pixels still blend at list position pos (vjp_tile's per-wave bounds) and the entry's
+// effective mask: its quadrant mask restricted to them.  A head entry is one with a non-empty effective mask.
+__device__ __forceinline__ uint32_t eff_mask(uint32_t e, uint32_t pos, const uint32_t* wm4) {
+  const uint32_t wb = (pos < wm4[0] ? 1u : 0u) | (pos < wm4[1] ? 2u : 0u) | (pos < wm4[2] ? 4u : 0u) |
+                      (pos < wm4[3] ? 8u : 0u);
+  return pl_mask(e) & wb;
 }
 
 // head flag of every sorted entry at its goff-order slot, and the goff slot itself in slots[k]
@@ -279,16 +285,17 @@ __global__ __launch_bounds__(256) void k_row_flags(int64_t N, int gx, const uint
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= N) return;
   const uint32_t t = keys[k];
-  const uint32_t g = pl_id(point_list[k]);
+  const uint32_t e = point_list[k];
+  const uint32_t g = pl_id(e);
   const uint32_t o = row_slot(goff[g], rect[g], (int)(t % (uint32_t)gx), (int)(t / (uint32_t)gx));
   slots[k] = o;
-  flags[o] = ((uint32_t)k - ranges[t].x) < neff[t] ? 1u : 0u;
+  flags[o] = eff_mask(e, (uint32_t)k - ranges[t].x, neff + 4 * (size_t)t) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void k_row_final(int64_t N, const uint32_t* __restrict__ hscan,
                                                     uint32_t* __restrict__ slots) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < N) slots[k] = hscan[slots[k]];  // tails get the next head's slot; they are never written
+  if (k < N) slots[k] = hscan[slots[k]];  // non-heads get the next head's slot; they are never written
 }
 
 int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,

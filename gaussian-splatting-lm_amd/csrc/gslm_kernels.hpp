@@ -405,7 +405,7 @@ struct BinBufs {
   uint32_t* slots;        // [N] gradient-row slot of each sorted entry, in the sort's free ping-pong key
                           // buffer: the LM row map (launch_lm_rowmap) once an LM product computed it for the
                           // current binning
-  uint32_t* tile_neff;    // [ntiles] largest n_contrib of each tile's pixels (the LM row map's head bound)
+  uint32_t* tile_neff;    // [4 ntiles] largest n_contrib of each tile quadrant's pixels (the LM row map's head bounds)
   int passes;
   int end_bit;
 };
@@ -422,8 +422,9 @@ struct ImgBufs {
 struct ScratchBufs {
   float4* trec;   // [P*3] tangent render records
   float4* contrib; // [N*3] per (tile, Gaussian) reduced gradient rows
-  // The LM row map: the rows of the LM tile passes exist only for HEAD entries (list position below the
-  // largest n_contrib of their tile -- every later entry's row would be zero).  hscan[o] = number of head
+  // The LM row map: the rows of the LM tile passes exist only for HEAD entries (their quadrant mask holds a
+  // quadrant whose largest n_contrib lies past their list position -- every other entry's row would be zero: no
+  // pixel still blending at that position can reach it).  hscan[o] = number of head
   // entries among the goff-order slots [0, o), o <= N, so Gaussian g's rows are [hscan[goff[g]],
   // hscan[goff[g] + tiles[g]]), contiguous; each sorted head entry's row slot is hscan of its goff slot.
   uint32_t* hscan;    // [N + 1]

@@ -171,6 +171,8 @@ constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * acc_st
 
 // Back-to-front pass over the tile's list (upstream BACKWARD::renderCUDA semantics), writing one
 // reduced row per (tile, Gaussian) pair.  Block-uniform control flow; requires blockDim = 256.
+// slots != NULL (the LM row map): rows exist for head entries only -- those some wave still blending at their list
+// position visits (a non-empty mask below) -- and the others are not written.
 template <bool WITH_XY, bool WITH_INV, int ROWF4, int BATCH>
 __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint2 range, const uint32_t* __restrict__ point_list,
@@ -335,7 +337,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       }
     }
     __syncthreads();
-    if (tid < cnt) {
+    if (tid < cnt && (!slots || my_mask)) {  // LM rows (slots): head entries only, see k_row_flags
       float t[NV];
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
