@@ -652,11 +652,21 @@ def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True, 
                      "view(s) (train_jvp.py:237-279; BASELINE configs[2], configs[3] at 8 GPUs)",
            "ms": 1e3 * t, "cg_iters": out["cg"]["iters"], "val_views": len(val_cams), "ranks": out["ranks"],
            "val_renders_per_rank": 7 * -(-len(val_cams) // out["ranks"]),
-           "loss_start": out["start_loss"], "loss_final": out["final_val_loss"], "best_alpha": out["best_alpha"]}
+           "loss_start": out["start_loss"], "loss_final": out["final_val_loss"], "best_alpha": out["best_alpha"],
+           "line_search": out["line_search"]}
     if with_timing:
-        o2 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart, timing=True)
+        # the phases, and the validation loss at the starting parameters (loss_start is the TRAINING view's loss: the
+        # line search's losses are over the validation views, so loss_val_start is the one loss_final compares with)
+        o2 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart, timing=True, val_at_start=True)
         restore()
-        res["breakdown_ms"] = o2["timing"]
+        res["breakdown_ms"] = {k: v for k, v in o2["timing"].items() if k != "val_start_ms"}
+        res["loss_val_start"] = o2["val_start_loss"]
+        res["ms_per_val_render"] = o2["timing"]["line_search_ms"] / res["val_renders_per_rank"]
+        # the same step with train_jvp.py's render order (update, render, ...: every render bins its view)
+        o3 = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart, timing=True, line_search="exact")
+        restore()
+        res["line_search_exact_ms"] = o3["timing"]["line_search_ms"]
+        res["exact_equal"] = (o3["trace"] == o2["trace"] and o3["final_val_loss"] == o2["final_val_loss"])
     return res
 
 

@@ -167,6 +167,39 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
                                  gb.counters, s, tiles_sorted);
 }
 
+// the line search's shared binning: the n parameter sets' geometries, and the union list's per-set masks
+int union_sets(const void* const* geoms, int32_t n, int64_t P, UnionSets* u) {
+  if (n < 1 || n > MAX_UNION_SETS) {
+    set_error("union: 1 <= n <= 8 parameter sets");
+    return GSLM_ERR_INVALID;
+  }
+  if (!geoms) { set_error("union: NULL geoms"); return GSLM_ERR_INVALID; }
+  *u = UnionSets{};
+  u->n = n;
+  for (int a = 0; a < n; ++a) {
+    if (!geoms[a] && P) { set_error("union: NULL geometry"); return GSLM_ERR_INVALID; }
+    GeomBufs gb;
+    geom_layout(P, const_cast<void*>(geoms[a]), &gb);
+    u->rec[a] = gb.rec;
+    u->tiles[a] = gb.tiles;
+    u->rect[a] = gb.rect;
+  }
+  return GSLM_OK;
+}
+
+size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* o) {
+  BinBufs bb;
+  const size_t off = bin_layout(N, ntiles, nullptr, &bb);
+  Carver c{(char*)binning};
+  c.off = off;
+  UnionMasks m;
+  m.m0 = c.take<uint32_t>(N);
+  m.m1 = c.take<uint32_t>(N);
+  m.sorted = (bb.passes & 1) ? m.m1 : m.m0;
+  if (o) *o = m;
+  return c.off;
+}
+
 }  // namespace gslm
 
 using namespace gslm;
@@ -340,6 +373,76 @@ int gslm_rasterize_loss_dev(const gslm_view* view, int64_t P, void* geom, void* 
   hipStream_t s = (hipStream_t)stream;
   if ((st = launch_binning(v, P, gb, bb, cap, s, true, n_out))) return st;
   return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0, s);
+}
+
+// ---- the line search's shared binning (ABI 8; forward.hip k_union_rect / k_duplicate_union) ----
+size_t gslm_union_binning_bytes(int64_t N, int32_t H, int32_t W) {
+  const int ntiles = ((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y);
+  return union_masks_layout(N, ntiles, nullptr, nullptr);
+}
+
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n,
+                        const uint32_t* depth_order, void* union_geom, size_t union_geom_bytes, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (P < 0 || P > MAX_P) { set_error("P out of range [0, 2^28 - 1]"); return GSLM_ERR_INVALID; }
+  if (union_geom_bytes < gslm_geom_bytes(P) || (!union_geom && P)) { set_error("union geometry workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (P && !depth_order) { set_error("union_geometry: NULL depth_order"); return GSLM_ERR_INVALID; }
+  UnionSets u;
+  if ((st = union_sets(geoms, n, P, &u))) return st;
+  GeomBufs ug;
+  geom_layout(P, union_geom, &ug);
+  hipStream_t s = (hipStream_t)stream;
+  if (P == 0) {
+    GSLM_HIP_CHECK(hipMemsetAsync(ug.counters, 0, 4, s));
+    return GSLM_OK;
+  }
+  if ((st = launch_union_rect(P, u, ug, s))) return st;
+  GSLM_HIP_CHECK(hipMemcpyAsync(ug.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+  // the union tile counts in depth order: k_duplicate_union's offsets, and the pair count in counters[0]
+  return exclusive_scan_u32(ug.tiles, ug.sorted_idx, ug.offsets, P, ug.scan_tmp, ug.counters, s);
+}
+
+int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,
+                       int64_t N, const void* const* geoms, int32_t n, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (P < 0 || P > MAX_P || N < 0 || N > 0xFFFFFFFFll) { set_error("union_binning: P or N out of range"); return GSLM_ERR_INVALID; }
+  if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (P && !union_geom) { set_error("union_binning: NULL union geometry"); return GSLM_ERR_INVALID; }
+  UnionSets u;
+  if ((st = union_sets(geoms, n, P, &u))) return st;
+  GeomBufs ug;
+  BinBufs bb;
+  UnionMasks um;
+  geom_layout(P, const_cast<void*>(union_geom), &ug);
+  bin_layout(N, v.gx * v.gy, binning, &bb);
+  union_masks_layout(N, v.gx * v.gy, binning, &um);
+  return launch_union_binning(v, P, ug, bb, um, N, u, (hipStream_t)stream);
+}
+
+int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, const void* binning,
+                             size_t binning_bytes, int64_t N, int32_t slot, const float* gt, const float* alpha_mask,
+                             void* scratch, size_t scratch_bytes, double* loss_dev, int32_t accumulate, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (slot < 0 || slot >= MAX_UNION_SETS) { set_error("rasterize_loss_slot: slot must be in [0, 8)"); return GSLM_ERR_INVALID; }
+  if (N < 0 || N > 0xFFFFFFFFll) { set_error("rasterize_loss_slot: N out of range"); return GSLM_ERR_INVALID; }
+  if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (scratch_bytes < gslm_loss_scratch_bytes(v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
+  if (!gt || !loss_dev || !scratch) { set_error("rasterize_loss_slot: NULL gt / loss / scratch"); return GSLM_ERR_INVALID; }
+  if (P && !geom) { set_error("rasterize_loss_slot: NULL geometry"); return GSLM_ERR_INVALID; }
+  GeomBufs gb;
+  BinBufs bb;
+  UnionMasks um;
+  geom_layout(P, const_cast<void*>(geom), &gb);
+  bin_layout(N, v.gx * v.gy, const_cast<void*>(binning), &bb);
+  union_masks_layout(N, v.gx * v.gy, const_cast<void*>(binning), &um);
+  return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0,
+                            (hipStream_t)stream, N > 0 ? um.sorted : nullptr, 4 * slot);
 }
 
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream) {
@@ -691,8 +794,10 @@ int gslm_gather_screen(const gslm_view* views, int32_t nviews, const gslm_gaussi
   ViewK vk[16];
   GaussK g;
   int st;
-  for (int b = 0; b < nviews; ++b)
+  for (int b = 0; b < nviews; ++b) {
     if ((st = make_view(&views[b], gi->max_coeffs, &vk[b]))) return st;
+    vk[b].stop = opts ? opts->cg_ctl : nullptr;  // a stopped solve's gather returns at once
+  }
   if ((st = make_gauss(gi, &vk[0], &g, false))) return st;
   if (!g.raw) { set_error("gather_screen: gaussians must be the raw GaussianModel leaves (raw = 1)"); return GSLM_ERR_INVALID; }
   const int32_t stages = (opts && opts->stages) ? opts->stages : GSLM_STAGE_ALL;
@@ -731,8 +836,10 @@ int gslm_tangent_views(const gslm_view* views, int32_t nviews, const gslm_gaussi
   ViewK vk[MAX_SCREEN_VIEWS];
   GaussK g;
   int st;
-  for (int b = 0; b < nviews; ++b)
+  for (int b = 0; b < nviews; ++b) {
     if ((st = make_view(&views[b], gi->max_coeffs, &vk[b]))) return st;
+    vk[b].stop = opts ? opts->cg_ctl : nullptr;  // a stopped solve's tangent records (and direction update) are skipped
+  }
   if ((st = make_gauss(gi, &vk[0], &g, false))) return st;
   if (!g.raw || g.cov3D || g.colors) {
     set_error("tangent_views: gaussians must be the raw GaussianModel leaves (raw = 1)");

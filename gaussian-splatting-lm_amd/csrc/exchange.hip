@@ -44,6 +44,7 @@ __global__ __launch_bounds__(256) void k_gather_screen(ViewsK vs, GaussK g, cons
                                                         int64_t sstride, FlatK o, RestK rc) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * rest width]
   __shared__ double s_dot[4];
+  if (cg_stopped(vs.v[0])) return;  // a stopped solve (gslm_matvec_opts.cg_ctl): block-uniform, before any barrier
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   ChainOut acc;
   acc.dop = 0.f;

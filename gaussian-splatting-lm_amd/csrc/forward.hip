@@ -318,6 +318,140 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
   return GSLM_OK;
 }
 
+// ---- the line search's shared binning (gslm_union_*) ----
+// The seven line-search points of train_jvp.py:262-280 differ only in the groups the LM step moves (xyz is masked,
+// :221-227), so one view's Gaussians keep their screen centre and depth order at every point and only their
+// footprints change.  Each point's exact point list -- the (tile, Gaussian) pairs of its rects in (tile, depth,
+// index) order -- is then the subsequence of ONE list binned over the union of the points' rects: the entries whose
+// tile lies in that point's rect.  k_duplicate_union gives every entry 4 bits per point: that point's quadrant mask
+// (quad_mask of its own record, the bits its exact k_duplicate would write) where the tile is in its rect, 0
+// elsewhere; the tile sort carries them with the pairs.  A blend that visits by those bits visits the exact list's
+// entries, in its order, with the same records: the same image and loss, bitwise (gslm_rasterize_loss_slot).
+
+// per Gaussian: the union of the rects of the sets where it is visible (tiles > 0), as the union geometry's tile
+// count and rect
+__global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint32_t* __restrict__ utiles,
+                                                     uint2* __restrict__ urect) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  uint32_t x0 = 0xFFFFu, y0 = 0xFFFFu, x1 = 0u, y1 = 0u;
+  for (int a = 0; a < u.n; ++a) {
+    if (u.tiles[a][i] == 0u) continue;
+    const uint2 rc = u.rect[a][i];
+    x0 = min(x0, rc.x & 0xFFFFu);
+    y0 = min(y0, rc.x >> 16);
+    x1 = max(x1, rc.y & 0xFFFFu);
+    y1 = max(y1, rc.y >> 16);
+  }
+  const bool any = x1 > x0 && y1 > y0;
+  utiles[i] = any ? (x1 - x0) * (y1 - y0) : 0u;
+  urect[i] = any ? make_uint2(x0 | (y0 << 16), x1 | (y1 << 16)) : make_uint2(0u, 0u);
+}
+
+// k_duplicate over the union rects (the same emission: one block per 256 Gaussians of the depth order, elements in
+// order, a Gaussian's rect row-major), the point-list quadrant bits 0xF, and amask[e] = bits 4a..4a+3 the quadrant
+// mask of set a.  Each set's record of the block's Gaussians is staged in LDS once ([x y a b], [c tq rect]: 32 B,
+// rect 0 when the set culls it) and the masks are evaluated per element.  Dynamic LDS: n * 256 * 32 B.
+__global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
+                                                          const uint32_t* __restrict__ offsets, uint32_t N,
+                                                          const uint2* __restrict__ urect, UnionSets u,
+                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                          uint32_t* __restrict__ amask) {
+  extern __shared__ float4 s_set[];  // [n][2][256]
+  __shared__ uint32_t s_off[257];
+  __shared__ uint32_t s_g[256];
+  __shared__ uint32_t s_rc[256][3];  // x0, y0, width of the union rect
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
+  const int64_t slast = min(s0 + 255, P - 1);
+  const uint32_t base = offsets[s0];
+  uint32_t n = 0;
+  if (s < P) {
+    const uint32_t g = sorted_idx[s];
+    const uint32_t o = offsets[s];
+    n = (s + 1 < P ? offsets[s + 1] : N) - o;
+    s_off[tid] = o - base;
+    if (n) {
+      const uint2 rc = urect[g];
+      const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
+      s_rc[tid][0] = (uint32_t)x0;
+      s_rc[tid][1] = (uint32_t)y0;
+      s_rc[tid][2] = (uint32_t)(x1 - x0);
+      s_g[tid] = g;
+      for (int a = 0; a < u.n; ++a) {
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+        if (u.tiles[a][g] != 0u) {
+          const float4* r = u.rec[a] + RECS * (size_t)g;
+          const float4 r3 = r[3];
+          r0 = r[0];
+          r1 = make_float4(r[1].x, r[2].w, r3.x, r3.y);
+        }
+        s_set[(2 * a) * 256 + tid] = r0;
+        s_set[(2 * a + 1) * 256 + tid] = r1;
+      }
+    }
+  } else {
+    s_off[tid] = 0xFFFFFFFFu;  // past the block's last Gaussian: never an owner
+  }
+  if (s == slast) s_off[256] = offsets[s] - base + n;
+  __syncthreads();
+  const uint32_t total = base < N ? min(s_off[256], N - base) : 0u;
+  for (uint32_t e = tid; e < total; e += 256) {
+    int lo = 0;
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1) lo = s_off[lo + step] <= e ? lo + step : lo;
+    const uint32_t li = e - s_off[lo];
+    const uint32_t w = s_rc[lo][2];
+    const uint32_t dy = li / w;
+    const int tx = (int)(s_rc[lo][0] + (li - dy * w)), ty = (int)(s_rc[lo][1] + dy);
+    uint32_t m = 0u;
+    for (int a = 0; a < u.n; ++a) {
+      const float4 r0 = s_set[(2 * a) * 256 + lo], r1 = s_set[(2 * a + 1) * 256 + lo];
+      const uint32_t rlo = __float_as_uint(r1.z), rhi = __float_as_uint(r1.w);
+      if (tx < (int)(rlo & 0xFFFFu) || ty < (int)(rlo >> 16) || tx >= (int)(rhi & 0xFFFFu) || ty >= (int)(rhi >> 16))
+        continue;  // outside set a's rect (an empty rect when set a culls the Gaussian)
+      m |= quad_mask(quad_cull_prep(r0.x, r0.y, r0.z, r0.w, r1.x, r1.y), tx, ty) << (4 * a);
+    }
+    keys[base + e] = (uint32_t)(ty * gx + tx);
+    vals[base + e] = s_g[lo] | (0xFu << ID_BITS);
+    amask[base + e] = m;
+  }
+}
+
+int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s) {
+  if (P <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_union_rect, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, u, ug.tiles, ug.rect);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
+int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,
+                         int64_t N, const UnionSets& u, hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
+  if (P > 0 && N > 0) {
+    const size_t lds = (size_t)u.n * 2 * 256 * sizeof(float4);
+    hipLaunchKernelGGL(k_duplicate_union, dim3((unsigned)((P + 255) / 256)), dim3(256), lds, s, P, v.gx, ug.sorted_idx,
+                       ug.offsets, (uint32_t)N, ug.rect, u, bb.keys0, bb.vals0, um.m0);
+    GSLM_LAUNCH_CHECK();
+    bool alt = false;
+    int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s, false, nullptr,
+                              nullptr, um.m0, um.m1);
+    if (st != GSLM_OK) return st;
+    if ((alt ? bb.vals1 : bb.vals0) != bb.point_list || (alt ? um.m1 : um.m0) != um.sorted) {
+      set_error("internal: radix pass count disagrees with the union binning layout");
+      return GSLM_ERR_INVALID;
+    }
+    const unsigned nbN = (unsigned)((N + 255) / 256);
+    hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, (const uint32_t*)nullptr,
+                       (uint32_t*)nullptr);
+    GSLM_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 // ------------------------------------------------------------------ launchers
 // k_preprocess_dma (default) or the register-staged k_preprocess: GSLM_PREPROCESS_STAGING=reg selects the latter
 // (an A/B switch; both write the bitwise same records)

@@ -58,9 +58,12 @@ inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_b
 // ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
 // last_gather (or NULL): the last pass writes last_gather[value] in place of each sorted key.
 // n_dev (or NULL): n is a capacity (grid and hist sized for it) and the kernels sort the first min(n, *n_dev) pairs.
+// p0 / p1 (or NULL): a second value array (p0 input, p1 its ping-pong partner) moved with the pairs; the result is
+// in p1 exactly when *result_in_alt.
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
                      uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false,
-                     const uint32_t* last_gather = nullptr, const uint32_t* n_dev = nullptr);
+                     const uint32_t* last_gather = nullptr, const uint32_t* n_dev = nullptr, uint32_t* p0 = nullptr,
+                     uint32_t* p1 = nullptr);
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;

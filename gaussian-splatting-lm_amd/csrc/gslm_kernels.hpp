@@ -444,8 +444,30 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
 int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, const ScratchBufs& sb,
                      int64_t N, hipStream_t s);
 int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipStream_t s);
+// amask (or NULL): the blend visits by the union list's per-set masks (bits `shift` .. shift + 3 of amask[k],
+// k_duplicate_union) with the records of gb (that set's geometry) instead of the point list's own quadrant bits
 int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
-                       double* part, double* loss, int accumulate, hipStream_t s);
+                       double* part, double* loss, int accumulate, hipStream_t s, const uint32_t* amask = nullptr,
+                       int shift = 0);
+// ---- the line search's shared binning (forward.hip, gslm_union_*) ----
+constexpr int MAX_UNION_SETS = 8;  // 4 mask bits per set in one uint32 per list entry
+struct UnionSets {
+  const float4* rec[MAX_UNION_SETS];
+  const uint32_t* tiles[MAX_UNION_SETS];
+  const uint2* rect[MAX_UNION_SETS];
+  int n;
+};
+// the union list's per-entry set masks: the tile sort's ping-pong pair after the binning layout; `sorted` is the one
+// holding the result (the same pass parity as the point list)
+struct UnionMasks {
+  uint32_t* m0;
+  uint32_t* m1;
+  uint32_t* sorted;
+};
+size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* out);
+int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s);
+int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,
+                         int64_t N, const UnionSets& u, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,
                       float* out_invdepth, hipStream_t s);
 

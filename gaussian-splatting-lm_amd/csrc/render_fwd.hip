@@ -21,14 +21,17 @@ namespace gslm {
 // arithmetic), sum r^2 in double per tile -> part[tile] (gslm_rasterize_loss).
 enum { FWD_FULL = 0, FWD_NO_INV = 1, FWD_LOSS = 2 };
 
-template <int MODE>
+// SLOT (FWD_LOSS only): the line search's union list (gslm_rasterize_loss_slot) -- an entry is visited by its set's
+// bits of amask (k_slot_masks: the set's own quadrant mask, 0 outside the set's rect) instead of the point list's.
+template <int MODE, bool SLOT = false>
 __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* __restrict__ ranges,
                                                           const uint32_t* __restrict__ tile_order,
                                                           const uint32_t* __restrict__ point_list,
                                                           const float4* __restrict__ rec, float* __restrict__ out_color,
                                                           float* __restrict__ out_invdepth, float* __restrict__ final_T,
                                                           uint32_t* __restrict__ n_contrib, const float* __restrict__ gt,
-                                                          const float* __restrict__ mask, double* __restrict__ part) {
+                                                          const float* __restrict__ mask, double* __restrict__ part,
+                                                          const uint32_t* __restrict__ amask = nullptr, int shift = 0) {
   __shared__ float4 s_rec[4][3 * 64];
   const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
     bool hit = false;
     if (k < n) {
       const uint32_t e = pl[k];
-      if ((pl_mask(e) >> q) & 1u) {
+      if (((SLOT ? amask[range.x + k] >> shift : pl_mask(e)) >> q) & 1u) {
         hit = true;
         const uint32_t g = pl_id(e);
         s[lane] = rec[RECS * (size_t)g + 0];
@@ -144,27 +147,32 @@ int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) return GSLM_OK;
   if (out_invdepth)
-    hipLaunchKernelGGL(k_render_fwd_wave<FWD_FULL>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+    hipLaunchKernelGGL((k_render_fwd_wave<FWD_FULL, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, out_color, out_invdepth, ib.final_T, ib.n_contrib, (const float*)nullptr,
-                       (const float*)nullptr, (double*)nullptr);
+                       (const float*)nullptr, (double*)nullptr, (const uint32_t*)nullptr, 0);
   else
-    hipLaunchKernelGGL(k_render_fwd_wave<FWD_NO_INV>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
+    hipLaunchKernelGGL((k_render_fwd_wave<FWD_NO_INV, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, out_color, (float*)nullptr, ib.final_T, ib.n_contrib, (const float*)nullptr,
-                       (const float*)nullptr, (double*)nullptr);
+                       (const float*)nullptr, (double*)nullptr, (const uint32_t*)nullptr, 0);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
 
 int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
-                       double* part, double* loss, int accumulate, hipStream_t s) {
+                       double* part, double* loss, int accumulate, hipStream_t s, const uint32_t* amask, int shift) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) {
     if (!accumulate) GSLM_HIP_CHECK(hipMemsetAsync(loss, 0, sizeof(double), s));
     return GSLM_OK;
   }
-  hipLaunchKernelGGL(k_render_fwd_wave<FWD_LOSS>, dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
-                     bb.point_list, gb.rec, (float*)nullptr, (float*)nullptr, (float*)nullptr, (uint32_t*)nullptr, gt,
-                     mask, part);
+  if (amask)
+    hipLaunchKernelGGL((k_render_fwd_wave<FWD_LOSS, true>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges,
+                       bb.tile_order, bb.point_list, gb.rec, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (uint32_t*)nullptr, gt, mask, part, amask, shift);
+  else
+    hipLaunchKernelGGL((k_render_fwd_wave<FWD_LOSS, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges,
+                       bb.tile_order, bb.point_list, gb.rec, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (uint32_t*)nullptr, gt, mask, part, (const uint32_t*)nullptr, 0);
   hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const double*)part, ntiles, accumulate, loss);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;

@@ -95,15 +95,19 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // counts into local positions: block order = wave order, round order, lane order = input order (stable).  The
 // keys are reordered through LDS into digit runs and each run is written to its global offset by consecutive
 // threads (coalesced segments instead of one scattered 4-byte store per key).
-template <int ITEMS>
+// PAY: a second value array moves with the pairs (pin -> pout; the line search's union list carries each entry's
+// per-set quadrant masks through the tile sort, gslm_union_binning).
+template <int ITEMS, bool PAY = false>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
-    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather, const uint32_t* __restrict__ n_dev) {
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather, const uint32_t* __restrict__ n_dev,
+    const uint32_t* __restrict__ pin = nullptr, uint32_t* __restrict__ pout = nullptr) {
   static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
   constexpr int TILE = SORT_THREADS * ITEMS;
   constexpr int WAVE_KEYS = TILE / 4;
   __shared__ uint32_t s_keys[TILE], s_vals[TILE];
+  __shared__ uint32_t s_pay[PAY ? TILE : 1];
   __shared__ uint32_t s_wcnt[4][RADIX];  // per-wave running digit count, then the wave's offset in the digit run
   __shared__ uint32_t s_loc[RADIX];      // block-local start of each digit's run
   __shared__ uint32_t s_gbase[RADIX];    // global offset of this block's run of each digit
@@ -120,11 +124,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   wave_order_lds();  // the zeroes before any lane's first counter read
   // all loads first (16 keys + 16 values per lane in flight), wave w on keys [wbase, wbase + 1024) of the block
   uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
+  uint32_t pay[PAY ? ITEMS : 1];
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const int64_t i = base + wbase + r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
     val[r] = i < n ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == NULL: the values are the indices
+    if (PAY) pay[r] = i < n ? pin[i] : 0u;
   }
   {
     // global base of each digit's run for this block = exclusive prefix of digit totals + this block's offset
@@ -174,6 +180,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
       const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
       s_keys[lp] = key[r];
       s_vals[lp] = val[r];
+      if (PAY) s_pay[lp] = pay[r];
     }
   }
   __syncthreads();
@@ -187,6 +194,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     // kgather[value] in sorted order instead (the tile counts the depth-order scan reads, gathered once here)
     kout[pos] = kgather ? kgather[val] : k;
     vout[pos] = val;
+    if (PAY) pout[pos] = s_pay[e];
   }
 }
 
@@ -376,13 +384,14 @@ int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* o
 
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
                      uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values, const uint32_t* last_gather,
-                     const uint32_t* n_dev) {
+                     const uint32_t* n_dev, uint32_t* p0, uint32_t* p1) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const int nb = (int)sort_blocks(n);
   const bool small = sort_items(n) != SORT_ITEMS;
   uint32_t* totals = hist + (size_t)RADIX * nb;
-  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1, *pi = p0, *po = p1;
+  const bool pay = p0 != nullptr;
   bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
   bool alt = false;
   // ceil(end_bit / 8) passes with the bits split evenly (13-bit tile ids: 7 + 6, not 8 + 5): fewer, longer
@@ -398,18 +407,27 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb,
                          n_dev);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-      hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift,
-                         nbits, hist, nb, totals, kg, n_dev);
+      if (pay)
+        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS_SMALL, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo,
+                           n, shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)pi, po);
+      else
+        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS_SMALL, false>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko,
+                           vo, n, shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
     } else {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb, n_dev);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-      hipLaunchKernelGGL(k_radix_scatter<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift, nbits,
-                         hist, nb, totals, kg, n_dev);
+      if (pay)
+        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
+                           shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)pi, po);
+      else
+        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, false>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
+                           shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
     }
     first = false;
     GSLM_LAUNCH_CHECK();
     std::swap(ki, ko);
     std::swap(vi, vo);
+    std::swap(pi, po);
     alt = !alt;
   }
   *result_in_alt = alt;

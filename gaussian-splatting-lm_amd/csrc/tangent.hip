@@ -167,6 +167,7 @@ __global__ __launch_bounds__(256) void k_tangent_views(ViewsK vs, GaussK g, Gaus
                                                         int64_t fstride, float4* __restrict__ out, int64_t ostride,
                                                         XpbyK xp, int compact, int view_base) {
   extern __shared__ __attribute__((aligned(16))) float s_rest[];  // [256 * 3(M-1)]
+  if (cg_stopped(vs.v[0])) return;  // a stopped solve (gslm_matvec_opts.cg_ctl): block-uniform, before any barrier
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + threadIdx.x;
   if (XPBY) {

@@ -110,6 +110,17 @@ EXPORTS = {
                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32,
                                                ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_num_rendered_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "gslm_union_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "gslm_union_geometry": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p]),
+    "gslm_union_binning": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.c_int32, ctypes.c_void_p]),
+    "gslm_rasterize_loss_slot": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int32,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "gslm_forward": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -205,7 +216,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 7  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 8  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):

@@ -814,6 +814,10 @@ class LossEvaluator:
         self.loss_scratch = [torch.empty(nb // 8 + 1, dtype=torch.float64, device=device) for _ in self.streams]
         self.num_rendered = [0] * len(cams)
         self._order_key, self._orders = None, [None] * len(cams)
+        # the shared binning of evaluate_points (gslm_union_*): per batch position k its sets' geometries, the union
+        # geometry and the union list
+        self.uslots = [dict(geoms=[], ugeom=None, binning=None) for _ in range(self.batch)]
+        self.union_counts = []
 
     def _slot(self, k, P):
         sl = self.slots[k]
@@ -860,10 +864,12 @@ class LossEvaluator:
         key = (xyz.data_ptr(), xyz._version, P)
         if key != self._order_key:  # xyz moved: sort again
             self._order_key, self._orders = key, [None] * V
-        for st in self.streams:  # the parameters (and the zeroed losses) as the main stream left them
+        # device-count renders' pair counts: allocated and zeroed on the main stream BEFORE the side streams wait on
+        # it, so no stream's k_ranges count write can precede the zero fill
+        counts = torch.zeros(max(V, 1), dtype=torch.int32, device=self.device)
+        for st in self.streams:  # the parameters (and the zeroed losses and counts) as the main stream left them
             if st is not None:
                 st.wait_stream(main)
-        counts = torch.zeros(max(V, 1), dtype=torch.int32, device=self.device)  # device-count renders' pair counts
         caps = {}  # view -> list capacity it was rendered with (device-count renders)
         for b0 in range(0, V, self.batch):
             idx = list(range(b0, min(V, b0 + self.batch)))
@@ -939,6 +945,116 @@ class LossEvaluator:
             self.reduce(loss)
         return loss
 
+    # ---- the line search's six points with one binning per view (include/gslm.h "shared binning", ABI 8) ----
+    def _ugeom(self, k, n, P):
+        sl = self.uslots[k]
+        nb = lib.gslm_geom_bytes(P)
+        while len(sl["geoms"]) < n:
+            sl["geoms"].append(None)
+        for a in range(n):
+            if sl["geoms"][a] is None or sl["geoms"][a].numel() < nb:
+                sl["geoms"][a] = _lib.u8(nb, self.device)
+        if sl["ugeom"] is None or sl["ugeom"].numel() < nb:
+            sl["ugeom"] = _lib.u8(nb, self.device)
+        return sl
+
+    def evaluate_points(self, sets):
+        """The validation loss at each of n <= 8 parameter sets (snapshots sharing the model's frozen xyz: the six
+        line-search points of train_jvp.py:262-277, param_snapshot), as a list of device doubles -- each bitwise equal
+        to evaluate() with the model at that set.  Per view: the n preprocesses (one depth order), ONE binning over the
+        union of the sets' rects (gslm_union_geometry / gslm_union_binning: 4 mask bits per set and list entry, carried
+        through the tile sort), then the n blends + losses through it (gslm_rasterize_loss_slot).  union_counts[i]:
+        view i's union list length (the last call)."""
+        n = len(sets)
+        if not 1 <= n <= 8:
+            raise ValueError("evaluate_points takes 1..8 parameter sets")
+        xyz = sets[0]._xyz
+        if any(st._xyz is not xyz for st in sets):
+            raise ValueError("evaluate_points: every set shares the frozen xyz tensor")
+        gs = [raw_gaussians(st) for st in sets]
+        P = gs[0].P
+        V = len(self.views)
+        main = torch.cuda.current_stream(self.device)
+        main_h = main.cuda_stream
+        key = (xyz.data_ptr(), xyz._version, P)
+        if key != self._order_key:
+            self._order_key, self._orders = key, [None] * V
+        losses = [torch.zeros(max(V, 1), dtype=torch.float64, device=self.device) for _ in range(n)]
+        self.union_counts = [0] * V
+        for st in self.streams:
+            if st is not None:
+                st.wait_stream(main)
+        for b0 in range(0, V, self.batch):
+            idx = list(range(b0, min(V, b0 + self.batch)))
+            slots = [self._ugeom(k, n, P) for k in range(len(idx))]
+            for k, (sl, i) in enumerate(zip(slots, idx)):
+                vw = self.views[i]
+                _, sh = self._stream(k)
+                mode0 = 2
+                if self._orders[i] is None:
+                    self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                    mode0 = 1
+                for a in range(n):
+                    check(lib.gslm_preprocess_ordered(ctypes.byref(vw), ctypes.byref(gs[a]), sl["geoms"][a].data_ptr(),
+                                                      sl["geoms"][a].numel(), None, self._orders[i].data_ptr(),
+                                                      mode0 if a == 0 else 2, sh), "gslm_preprocess_ordered")
+                ge = (ctypes.c_void_p * n)(*[sl["geoms"][a].data_ptr() for a in range(n)])
+                check(lib.gslm_union_geometry(ctypes.byref(vw), P, ge, n, self._orders[i].data_ptr(),
+                                              sl["ugeom"].data_ptr(), sl["ugeom"].numel(), sh), "gslm_union_geometry")
+            for st in self.streams:
+                if st is not None:
+                    main.wait_stream(st)
+            ugeoms = (ctypes.c_void_p * len(idx))(*[sl["ugeom"].data_ptr() for sl in slots])
+            Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
+            Ns = (ctypes.c_int64 * len(idx))()
+            check(lib.gslm_num_rendered_many(ugeoms, Ps, len(idx), Ns, main_h), "gslm_num_rendered_many")  # syncs
+            for k, (sl, i) in enumerate(zip(slots, idx)):
+                vw = self.views[i]
+                H, W, N = vw.image_height, vw.image_width, int(Ns[k])
+                self.union_counts[i] = N
+                st, sh = self._stream(k)
+                need = lib.gslm_union_binning_bytes(N, H, W)
+                if sl["binning"] is None or sl["binning"].numel() < need:
+                    if sl["binning"] is not None and st is not None:
+                        main.wait_stream(st)  # freed on the main stream: after its last use
+                    sl["binning"] = _lib.u8(int(need * 1.25) + 4096, self.device)
+                binning = sl["binning"]
+                ge = (ctypes.c_void_p * n)(*[sl["geoms"][a].data_ptr() for a in range(n)])
+                check(lib.gslm_union_binning(ctypes.byref(vw), P, sl["ugeom"].data_ptr(), binning.data_ptr(),
+                                             binning.numel(), N, ge, n, sh), "gslm_union_binning")
+                m = self.masks[i]
+                scr = self.loss_scratch[k % len(self.streams)]
+                for a in range(n):
+                    check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][a].data_ptr(), binning.data_ptr(),
+                                                       binning.numel(), N, a, self.gts[i].data_ptr(),
+                                                       None if m is None else m.data_ptr(), scr.data_ptr(),
+                                                       scr.numel() * 8, losses[a].data_ptr() + 8 * i, 0, sh),
+                          "gslm_rasterize_loss_slot")
+        for st in self.streams:
+            if st is not None:
+                main.wait_stream(st)
+        out = []
+        for a in range(n):
+            loss = losses[a][:V].sum() if V else losses[a][0]
+            if self.reduce is not None:
+                self.reduce(loss)
+            out.append(loss)
+        return out
+
+
+_LS_GROUPS = ("_features_dc", "_features_rest", "_scaling", "_rotation", "_opacity")
+
+
+def param_snapshot(model):
+    """A line-search point's parameters for LossEvaluator.evaluate_points: clones of the groups the LM step moves,
+    the model's own (frozen) xyz tensor.  The exposure group is not rendered by the validation loss."""
+    import types
+    ns = types.SimpleNamespace(_xyz=model._xyz, active_sh_degree=model.active_sh_degree)
+    with torch.no_grad():
+        for k in _LS_GROUPS:
+            setattr(ns, k, getattr(model, k).detach().clone())
+    return ns
+
 
 def update_params(model, layout, step, scale, skip_xyz=False):
     """GaussianModel.update_step(scale * s) (gaussian_model.py:131-139) from a flat step.  skip_xyz: the step's xyz
@@ -958,7 +1074,7 @@ def update_params(model, layout, step, scale, skip_xyz=False):
 
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
             verbose=False, device="cuda", sh_projection="auto", recursion="fused", exchange="auto", group=None,
-            val_batch=8, timing=False, backend=None):
+            val_batch=8, timing=False, backend=None, line_search="union", val_at_start=False):
     """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search.
 
     Single process: LMProblem over `cams` (with one training view the SH-rest group of the CG vectors is carried
@@ -972,6 +1088,11 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     reference's residual-space recursion; single process only).  check_every: the reference's stopping tests,
     on the device (cgls_fused).  timing=True adds wall-clock phases (evaluate + J^T b, CG, line search) to the
     result, synchronising the device at their boundaries.
+    line_search: "union" (xyz masked: the six points' parameters are formed first by the same update_step sequence
+    and their validation losses come from ONE binning per view, LossEvaluator.evaluate_points -- bitwise the losses of
+    the sequential renders; the final point, known only after them, is rendered as before) or "exact" (train_jvp.py's
+    order: update, render, update, ...).  val_at_start: also report the validation loss at the starting parameters
+    (one more evaluation, outside the reference's algorithm: it shows whether the step descends).
     backend: (problem_cls, evaluator_cls, solver) replacing (LMProblem, LossEvaluator, cgls_fused) -- the CPU
     multi-process tests run this same driver, sharding and reductions on the oracle restatement."""
     import time
@@ -1018,24 +1139,50 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     mine_val = [val_cams[i] for i in shard_views(len(val_cams), rank, n)] if sharded else val_cams
     val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
                         reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
+    val_start = float(val.evaluate()) if val_at_start else None
+    if val_at_start:
+        lap("val_start_ms")
+    if line_search not in ("union", "exact"):
+        raise ValueError(f"line_search must be 'union' or 'exact', got {line_search!r}")
+    union = line_search == "union" and mask_xyz and hasattr(val, "evaluate_points")
     # train_jvp.py:262-279: alpha = 2, 1, ..., 1/16 on the validation views, keep the best, step to it
     alpha = 2.0
     best_alpha, best_loss = alpha, math.inf
     trace = []
     update_params(model, full, s, alpha, skip_xyz=mask_xyz)
-    for _ in range(6):
-        vl = float(val.evaluate())
-        trace.append((alpha, vl))
-        if vl < best_loss:
-            best_loss, best_alpha = vl, alpha
-        new_alpha = alpha * 0.5
-        update_params(model, full, s, new_alpha - alpha, skip_xyz=mask_xyz)
-        alpha = new_alpha
+    if union:
+        # the same update_step sequence, the six points' parameters kept; their losses from one binning per view
+        points = []
+        for _ in range(6):
+            points.append((alpha, param_snapshot(model)))
+            new_alpha = alpha * 0.5
+            update_params(model, full, s, new_alpha - alpha, skip_xyz=mask_xyz)
+            alpha = new_alpha
+        alphas = [a for a, _ in points]
+        vls = [float(v) for v in val.evaluate_points([p for _, p in points])]
+        del points
+        for a, vl in zip(alphas, vls):
+            trace.append((a, vl))
+            if vl < best_loss:
+                best_loss, best_alpha = vl, a
+    else:
+        for _ in range(6):
+            vl = float(val.evaluate())
+            trace.append((alpha, vl))
+            if vl < best_loss:
+                best_loss, best_alpha = vl, alpha
+            new_alpha = alpha * 0.5
+            update_params(model, full, s, new_alpha - alpha, skip_xyz=mask_xyz)
+            alpha = new_alpha
     update_params(model, full, s, best_alpha - alpha, skip_xyz=mask_xyz)
     final = float(val.evaluate())
     lap("line_search_ms")
     out = dict(start_loss=start_loss, final_val_loss=final, best_alpha=best_alpha, cg=info, step=s, trace=trace,
-               val_views=len(val_cams), ranks=n if sharded else 1)
+               val_views=len(val_cams), ranks=n if sharded else 1, line_search="union" if union else "exact")
+    if val_at_start:
+        out["val_start_loss"] = val_start
+    if union and getattr(val, "union_counts", None):
+        out["union_pairs"] = sum(val.union_counts)
     if timing:
         out["timing"] = t
     return out

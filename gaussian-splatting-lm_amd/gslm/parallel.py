@@ -304,6 +304,21 @@ class GaussianShardedOperator:
             return
         _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
 
+    def _overlap(self):
+        """Whether the product's all-to-alls run asynchronously, overlapped with the tile passes of the other views
+        (a device backend: RCCL runs the collective on its own stream, ordered after the kernels enqueued before it
+        was issued; Work.wait() orders the compute stream after it).  gloo stages through the host: synchronous."""
+        if self._emulate or not collectives_on(self.world_size) or os.environ.get("GSLM_OVERLAP", "1") == "0":
+            return False
+        return dist.get_backend(self.group) == "nccl"
+
+    def _all_to_all_async(self, out, inp):
+        """all_to_all_single issued without waiting: the Work to wait on, or None once done (synchronous paths)."""
+        if self._overlap():
+            return dist.all_to_all_single(out, inp, group=self.group, async_op=True)
+        self._all_to_all(out, inp)
+        return None
+
     def allreduce_scalars(self, sc, slots):
         """Sum the CG scalars sc[slots] (device doubles, per-shard partials) over the ranks.  One slot (the CG
         loop's delta and gamma' without the residual monitor): in place on the 8-byte view, no gather / scatter
@@ -552,13 +567,23 @@ class GaussianShardedOperator:
             # empty shard: the direction update has nothing here but rank 0's exposure tail, which an empty
             # shard never holds (rank 0 owns Gaussians whenever P > 0)
             pre = None
-        # 1. tangent records of this shard for every view (direction update fused into the first call)
+        # The views are ordered b = k n + t (the k-th view of rank t), so view group k = [k n, (k + 1) n) is one
+        # all-to-all's worth.  With several views per rank the stages are pipelined over the groups (SURVEY 8(e)
+        # "overlap the reduce-scatter of view k's contribution with view k+1's JVP/VJP"): the records of group k are
+        # sent while group k+1's are written, view k renders while group k+1's records are in flight, and view k's
+        # screen sums are sent while view k+1 renders.  Same kernels, same buffers, same order of every sum: the
+        # products are bitwise those of the unpipelined schedule (GSLM_OVERLAP=0).
         R = self.rest_basis() if self.rest_views else None
-        for c0 in range(0, nv, chunk):
-            c1 = min(nv, c0 + chunk)
+        overlap = self._overlap() and per > 1
+        tchunk = n if overlap else chunk  # one tangent call per view group, its all-to-all issued at once
+        works = []
+        # 1. tangent records of this shard for every view (direction update fused into the first call)
+        for c0 in range(0, nv, tchunk):
+            c1 = min(nv, c0 + tchunk)
             opts = None
-            if (pre is not None and c0 == 0) or R is not None:
+            if (pre is not None and c0 == 0) or R is not None or cg_ctl is not None:
                 opts = _lib.GslmMatvecOpts()
+                opts.cg_ctl = cg_ctl  # a stopped solve's tangent kernel returns at once
             if pre is not None and c0 == 0:
                 keep.append(self._pre_opts(opts, v, pre))
             if R is not None:
@@ -569,13 +594,20 @@ class GaussianShardedOperator:
                                          b["trec_send"].data_ptr() + 32 * c0 * S, S,
                                          None if opts is None else ctypes.byref(opts), loc.stream),
                   "gslm_tangent_views")
+            if overlap:  # 2. (pipelined) every shard's records of my view of group c0 / n
+                k = c0 // n
+                works.append(self._all_to_all_async(b["trec_recv"][k], b["trec_send"][k]))
         self._mark(1)
         # 2. every shard's records of my k-th view
-        for k in range(per):
-            self._all_to_all(b["trec_recv"][k], b["trec_send"][k])
+        if not overlap:
+            for k in range(per):
+                self._all_to_all(b["trec_recv"][k], b["trec_send"][k])
         self._mark(2)
         # 3. render my views from the exchanged tables: per-Gaussian screen-space sums
+        swork = []
         for k, vr in enumerate(loc.views):
+            if overlap and works[k] is not None:
+                works[k].wait()  # the compute stream waits for view k's table only
             opts = _lib.GslmMatvecOpts()
             opts.stages = 2 | 16  # RENDER | SCREEN
             opts.flags = 1 if vr.tail_clean else 0  # GSLM_MV_TAIL_CLEAN
@@ -587,10 +619,17 @@ class GaussianShardedOperator:
                                           vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(), vr.scratch.numel(),
                                           ctypes.byref(vs), ctypes.byref(opts), loc.stream), "gslm_matvec_view_ex")
             vr.tail_clean = True
+            if overlap:  # 4. (pipelined) view k's screen sums leave while view k+1 renders
+                swork.append(self._all_to_all_async(b["screen_recv"][k], b["screen_send"][k]))
         self._mark(3)
         # 4. my shard's slices of every view's screen sums
-        for k in range(per):
-            self._all_to_all(b["screen_recv"][k], b["screen_send"][k])
+        if overlap:
+            for w in swork:
+                if w is not None:
+                    w.wait()
+        else:
+            for k in range(per):
+                self._all_to_all(b["screen_recv"][k], b["screen_send"][k])
         self._mark(4)
         # 5. every view's chain over my shard, + D v, <v, y>
         fuse = dot_out is not None and self.hi > self.lo
@@ -600,6 +639,7 @@ class GaussianShardedOperator:
             opts.stages = 7 | (8 if c0 == 0 else 0)
             opts.damp7 = self._damps if c0 == 0 else None
             opts.screen_stride = S
+            opts.cg_ctl = cg_ctl  # as the tangent and tile kernels: nothing runs once the solve has stopped
             if R is not None:
                 opts.rest_basis, opts.rest_views, opts.view_base = R.data_ptr(), self.rest_views, c0
             if fuse and c1 == nv:

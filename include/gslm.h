@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 7
+#define GSLM_ABI_VERSION 8
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -156,6 +156,31 @@ int gslm_rasterize_loss_dev(const gslm_view* view, int64_t P, void* geom, void* 
                             double* loss_dev, int32_t accumulate, uint32_t* n_out, void* stream);
 /* Stream-ordered 4-byte copy of gslm_preprocess' pair count to dst (device or host-pinned); no synchronisation. */
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream);
+
+/* ---- The line search's shared binning (ABI 8) ----
+ * train_jvp.py:262-277 renders every validation view at six points theta + alpha s (alpha = 2, 1, .., 1/16) of one step
+ * s whose xyz group is masked (:221-227).  A view's Gaussians then keep their screen centre and depth order at every
+ * point, and each point's exact point list is the subsequence of one list binned over the union of the points' rects:
+ * the entries whose tile lies in that point's rect, in the same (tile, depth, index) order.  So a view is binned once
+ * for the six points instead of once per point (gslm.lm.LossEvaluator.evaluate_points):
+ *   1. gslm_preprocess_ordered of each point's parameters into its own geometry workspace (geoms[a], one depth order);
+ *   2. gslm_union_geometry: the union of the n <= 8 points' rects per Gaussian into union_geom, its tile counts scanned
+ *      in depth order -- gslm_num_rendered(union_geom) is the union list's length N;
+ *   3. gslm_union_binning (workspace >= gslm_union_binning_bytes(N, H, W)): duplicate + tile sort + ranges of the union
+ *      list, each entry carrying 4 bits per point through the sort (slot a: the point's quadrant mask of the entry --
+ *      the bits its own binning would give it -- and 0 when its tile is outside the point's rect or the Gaussian is
+ *      culled there);
+ *   4. gslm_rasterize_loss_slot(geom = geoms[a], slot = a): gslm_rasterize_loss's blend + loss over the entries of
+ *      slot a -- the same visits in the same order with the same records as the exact render: the same loss, bitwise. */
+size_t gslm_union_binning_bytes(int64_t num_rendered, int32_t H, int32_t W);
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n,
+                        const uint32_t* depth_order, void* union_geom, size_t union_geom_bytes, void* stream);
+int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,
+                       int64_t num_rendered, const void* const* geoms, int32_t n, void* stream);
+int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, const void* binning,
+                             size_t binning_bytes, int64_t num_rendered, int32_t slot, const float* gt,
+                             const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
+                             int32_t accumulate, void* stream);
 /* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
  * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
  * gslm_rasterize with a larger buffer). */
@@ -258,7 +283,8 @@ typedef struct gslm_matvec_opts {
   /* Device CG control block of gslm_cg_monitor, or NULL: when cg_ctl[0] != 0 (the solve's stopping tests have
    * fired) the TANGENT, RENDER and GATHER kernels of this call return without work (and without writing y,
    * the dot or the direction update), so a host can enqueue a whole CGLS schedule without reading the tests
-   * back each iteration. */
+   * back each iteration.  gslm_matvec_view_ex, gslm_tangent_views and gslm_gather_screen (the Gaussian-sharded
+   * exchange's stages) all honour it. */
   const double* cg_ctl;
   /* gslm_tangent_views / gslm_gather_screen only (ABI 6): SH-rest coordinates of the Gaussian-sharded exchange.
    * When rest_basis is set, the SH-rest group of v, y (and of the fused direction update's s) holds 3 rest_views

@@ -147,6 +147,23 @@ class OracleLossEvaluator:
             self.reduce(loss)
         return loss
 
+    def evaluate_points(self, sets):
+        """gslm.lm.LossEvaluator.evaluate_points' interface: the loss at each parameter snapshot (gslm.lm.param_snapshot),
+        the model's leaves swapped for the snapshot's while it renders."""
+        m = self.prob.model
+        names = ("_features_dc", "_features_rest", "_scaling", "_rotation", "_opacity")
+        saved = [getattr(m, k) for k in names]
+        out = []
+        try:
+            for st in sets:
+                for k in names:
+                    setattr(m, k, getattr(st, k))
+                out.append(self.evaluate())
+        finally:
+            for k, t in zip(names, saved):
+                setattr(m, k, t)
+        return out
+
 
 def cgls_solver(op, g, max_iter=10, restart_iter=10, check_every=True, verbose=False):
     """cgls_ref in gslm.lm.lm_step's solver interface: (x, info)."""

@@ -1,0 +1,154 @@
+"""GPU: the line search with one binning per validation view and LM step (ABI 8, include/gslm.h "shared binning";
+gslm.lm.LossEvaluator.evaluate_points).
+
+train_jvp.py:262-277 renders every validation view at six points theta + alpha s with xyz masked (:221-227).  The
+union path bins each view once over the union of the points' rects and blends every point through that list with
+its own per-entry quadrant bits (carried through the tile sort).  The claim is exactness, so every comparison here is `==` against the exact renders
+(gslm_rasterize_loss with the point's own binning, LossEvaluator.evaluate), not a tolerance:
+  * each of the six points' losses, with steps large enough that radii and rects change between points, at 320x208
+    and at 1080p / 200k Gaussians, over several batch and stream counts;
+  * alpha masks, and points that cull Gaussians others keep (empty quadrant masks, zero-area rects);
+  * lm_step(line_search="union") against lm_step(line_search="exact"): trace, best_alpha, final loss and the
+    stepped parameters bitwise, and the reference-solver golden (test_gpu_lm_step.py) through the union path.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _scene(P=20000, W=320, H=208, nviews=5, seed=0, D=3, s0=0.01):
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    m = synthetic_gaussians(P, D, seed=seed, s0=s0).to("cuda")
+    cams = orbit_cameras(nviews, W, H, seed=7)
+    for i, c in enumerate(cams):
+        c.original_image = torch.rand(3, H, W, generator=torch.Generator().manual_seed(60 + i))
+        c.to("cuda")
+    return m, cams
+
+
+def _step(m, seed=3, scale=1.0):
+    """A step on every group but xyz, large enough that scales (hence radii and rects) and opacities (hence quadrant
+    masks) differ between the line-search points."""
+    from gslm.params import ParamLayout
+    P, K = m._xyz.shape[0], 1 + m._features_rest.shape[1]
+    lay = ParamLayout(P, K, m._exposure.shape[0])
+    s = torch.zeros(lay.numel, device="cuda")
+    v = lay.views(s)
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    for name, sd in (("features_dc", 0.1), ("features_rest", 0.02), ("scaling", 0.25), ("rotation", 0.2),
+                     ("opacity", 0.8)):
+        v[name].copy_(scale * sd * torch.randn(v[name].shape, generator=gen, device="cuda"))
+    return lay, s
+
+
+def _points(m, lay, s, ev_exact):
+    """The six points as lm_step forms them, with each point's exact loss and pair counts."""
+    from gslm.lm import param_snapshot, update_params
+    alpha = 2.0
+    update_params(m, lay, s, alpha, skip_xyz=True)
+    sets, exact, counts = [], [], []
+    for _ in range(6):
+        sets.append(param_snapshot(m))
+        exact.append(float(ev_exact.evaluate()))
+        counts.append(list(ev_exact.num_rendered))
+        update_params(m, lay, s, 0.5 * alpha - alpha, skip_xyz=True)
+        alpha *= 0.5
+    return sets, exact, counts, alpha
+
+
+@pytest.mark.parametrize("batch,streams", [(2, 2), (8, 8), (1, 1)])
+def test_evaluate_points_equal_exact_renders(batch, streams):
+    from gslm.lm import LossEvaluator
+    m, cams = _scene()
+    lay, s = _step(m)
+    ev_x = LossEvaluator(m, cams, torch.zeros(3), batch=batch, streams=streams)
+    ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=batch, streams=streams)
+    sets, exact, counts, alpha = _points(m, lay, s, ev_x)
+    got = [float(x) for x in ev_u.evaluate_points(sets)]
+    assert got == exact
+    # the union list holds every point's list and is longer than some (the test moves rects)
+    for i, N in enumerate(ev_u.union_counts):
+        assert N >= max(c[i] for c in counts)
+    assert any(N > min(c[i] for c in counts) for i, N in enumerate(ev_u.union_counts))
+    # fewer points, and a second LM step on the same evaluator (buffers reused, depth orders cached)
+    assert [float(x) for x in ev_u.evaluate_points(sets[2:5])] == exact[2:5]
+    sets2, exact2, _, _ = _points(m, lay, s, ev_x)
+    assert [float(x) for x in ev_u.evaluate_points(sets2)] == exact2
+
+
+def test_evaluate_points_with_alpha_masks_and_culled_sets():
+    """Alpha masks on the residual, and points where some Gaussians are culled (opacity driven below 1/255, so their
+    quadrant masks are empty, and scales driven to zero-area rects) while other points keep them."""
+    from gslm.lm import LossEvaluator, param_snapshot
+    m, cams = _scene(nviews=3)
+    masks = [(torch.rand(1, c.image_height, c.image_width, generator=torch.Generator().manual_seed(9 + i)) > 0.3).float()
+             for i, c in enumerate(cams)]
+    ev_x = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2, alpha_masks=masks)
+    ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2, alpha_masks=masks)
+    sets, exact = [], []
+    for k in range(4):
+        with torch.no_grad():
+            m._opacity[k::4] -= 12.0      # below the 1/255 cut: reaches no pixel
+            m._scaling[(k + 1)::4] += 0.7  # larger footprints
+            m._scaling[(k + 2)::9] -= 9.0  # vanishing footprints
+        sets.append(param_snapshot(m))
+        exact.append(float(ev_x.evaluate()))
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+
+
+def test_evaluate_points_1080p_200k():
+    """At the bench's resolution (1080p, 200k Gaussians at the bench's footprint scale, 3 views): every point equal."""
+    from gslm.lm import LossEvaluator
+    m, cams = _scene(P=200_000, W=1920, H=1080, nviews=3, s0=0.005)
+    lay, s = _step(m, seed=11, scale=0.5)
+    ev_x = LossEvaluator(m, cams, torch.zeros(3))
+    ev_u = LossEvaluator(m, cams, torch.zeros(3))
+    sets, exact, _, _ = _points(m, lay, s, ev_x)
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+
+
+def test_lm_step_union_equals_exact_line_search():
+    from gslm.cameras import orbit_cameras
+    from gslm.lm import lm_step
+    from gslm.model import synthetic_gaussians
+    outs, params = [], []
+    for ls in ("union", "exact"):
+        m = synthetic_gaussians(30000, 3, seed=0, s0=0.01).to("cuda")
+        cams = orbit_cameras(1, 320, 208, seed=1)
+        val = orbit_cameras(6, 320, 208, seed=4)
+        for i, c in enumerate(cams + val):
+            c.original_image = torch.rand(3, 208, 320, generator=torch.Generator().manual_seed(80 + i))
+            c.to("cuda")
+        outs.append(lm_step(m, cams, val, torch.zeros(3), max_iter=10, restart_iter=10, line_search=ls,
+                            val_at_start=True))
+        params.append([t.detach().clone() for t in (m._features_dc, m._features_rest, m._scaling, m._rotation,
+                                                     m._opacity, m._xyz)])
+    u, x = outs
+    assert u["line_search"] == "union" and x["line_search"] == "exact"
+    assert u["trace"] == x["trace"]
+    assert u["best_alpha"] == x["best_alpha"]
+    assert u["final_val_loss"] == x["final_val_loss"]
+    assert u["val_start_loss"] == x["val_start_loss"]
+    for a, b in zip(*params):
+        assert torch.equal(a, b)
+
+
+def test_union_lm_step_matches_reference_golden():
+    """The reference-solver golden of test_gpu_lm_step.py, through the union line search (lm_step's default)."""
+    import test_gpu_lm_step as t
+    d, L, m, cams, val = t._setup()
+    from gslm.lm import lm_step
+    out = lm_step(m, cams, val, torch.zeros(3), max_iter=10, restart_iter=10, check_every=True, line_search="union")
+    assert out["line_search"] == "union"
+    assert out["best_alpha"] == float(L["ten_best_alpha"])
+    losses = np.array([v for _, v in out["trace"]])
+    ref = L["ten_trace_loss"]
+    assert np.abs(losses - ref).max() <= 1e-4 * ref.max()
+    fin = float(L["ten_final_val_loss"])
+    assert abs(out["final_val_loss"] - fin) <= 1e-4 * fin
