@@ -245,6 +245,27 @@ int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* gi, voi
   return do_preprocess(v, g, gb, out_radii, (hipStream_t)stream, depth_order, order_mode);
 }
 
+int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, void* const* geoms,
+                          size_t geom_bytes, void* stream) {
+  if (!views || !gi || !geoms || nviews < 1 || nviews > MAX_PRE_VIEWS) {
+    set_error("preprocess_views: NULL argument or nviews outside 1..8");
+    return GSLM_ERR_INVALID;
+  }
+  PreViewsK pv;
+  GeomBufs gbs[MAX_PRE_VIEWS];
+  GaussK g;
+  int st;
+  for (int b = 0; b < nviews; ++b) {
+    if ((st = make_view(&views[b], gi->max_coeffs, &pv.v[b]))) return st;
+    if ((st = make_gauss(gi, &pv.v[b], &g, false))) return st;  // each view's SH degree against the stored coefficients
+    if (geom_bytes < gslm_geom_bytes(g.P) || (!geoms[b] && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
+    geom_layout(g.P, geoms[b], &gbs[b]);
+    pv.out[b] = PreOutBufs{gbs[b].rec, gbs[b].depth_key, gbs[b].tiles, gbs[b].rect, gbs[b].clampw};
+  }
+  pv.n = nviews;
+  return launch_preprocess_views(pv, g, gbs, (hipStream_t)stream);
+}
+
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
   GeomBufs gb;
   geom_layout(P, const_cast<void*>(geom), &gb);

@@ -167,8 +167,11 @@ __device__ __forceinline__ double rest_gram(const float A[16], const float B[16]
 }
 
 // One thread per Gaussian: the Gram matrix G[a][b] = <B_a, B_b> of the V views' SH-rest vectors (double), its
-// upper Cholesky factor column by column (G = R^T R, i.e. Gram-Schmidt of B_0, B_1, .. in view order), a view
-// adding less than 1e-6 of its norm to the earlier ones' span dropped (row zeroed), R packed by columns.
+// upper Cholesky factor column by column (G = R^T R, i.e. Gram-Schmidt of B_0, B_1, .. in view order), R packed by
+// columns (float).  A view adding less than sqrt(1e-7) = 3.2e-4 of its norm to the earlier ones' span is dropped (row
+// zeroed): gslm_rest_coords divides by the float R[b][b], so a kept view's relative R[b][b] bounds how far the float
+// rounding of R (6e-8) is amplified -- at most ~2e-4 here (a 1e-6 cut, round 3, allowed ~6%), and a dropped view's
+// part outside the span is below 3.2e-4 of its direction.
 __global__ __launch_bounds__(256) void k_rest_basis(ViewsK vs, GaussK g, float* __restrict__ R) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.P) return;
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(256) void k_rest_basis(ViewsK vs, GaussK g, float* 
         Rm[j][b] = r;
         d -= r * r;
       }
-    Rm[b][b] = (gbb > 0.0 && d > 1e-12 * gbb) ? sqrt(d) : 0.0;
+    Rm[b][b] = (gbb > 0.0 && d > 1e-7 * gbb) ? sqrt(d) : 0.0;
 #pragma unroll
     for (int j = 0; j < MAX_REST_VIEWS; ++j)
       if (j <= b) out[rest_basis_floats(b) + j] = (float)Rm[j][b];

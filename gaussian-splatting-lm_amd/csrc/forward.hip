@@ -138,6 +138,94 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
   if (radii_out) radii_out[i] = o.radius;
 }
 
+// k_preprocess_dma for up to MAX_PRE_VIEWS views in one pass over the Gaussians (gslm_preprocess_views: the line
+// search's parameter sets over a batch of validation views).  A view's inputs cost 236 B per Gaussian at SH 3 against
+// 84 B of its outputs; the block loads its Gaussians' inputs and stages their SH rows once, then writes every view's
+// records, depth keys, tile counts and rects from them.  Per view the same functions in the same order as
+// k_preprocess_dma: bitwise the same geometry.
+template <bool RAW>
+__global__ __launch_bounds__(256) void k_preprocess_views(PreViewsK pv, GaussK g) {
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];  // [256 * rest_stride]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + tid;
+  const bool live = i < g.P;
+  PreIn in{};
+  if (live) load_pre_in<RAW>(g, i, in);
+  asm volatile("" : : "v"(in.x), "v"(in.y), "v"(in.z), "v"(in.c[0]), "v"(in.c[1]), "v"(in.c[2]), "v"(in.c[3]),
+               "v"(in.c[4]), "v"(in.c[5]), "v"(in.qw), "v"(in.op));
+  const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+  const int64_t total = nv * g.rest_stride;
+  const int64_t n4 = total / 4;
+  const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+  float4* dst4 = reinterpret_cast<float4*>(s_sh);
+  for (int64_t c = w; c * 64 < n4; c += 4) {
+    const int64_t e = min(c * 64 + lane, n4 - 1);
+    glds16(src4 + e, dst4 + c * 64);
+  }
+  // view 0's geometry while the rows land (as k_preprocess_dma)
+  PreOut o0;
+  o0.depth = 0.f;
+  const bool vis0 = live && preprocess_core<RAW, false>(pv.v[0], g, i, in, o0);
+  __syncthreads();
+  if (n4 * 4 < total) {
+    for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+    __syncthreads();
+  }
+  if (!live) return;
+  g.rest = s_sh;
+  g.rest_base = i0;
+#pragma unroll 1
+  for (int b = 0; b < pv.n; ++b) {
+    const ViewK& v = pv.v[b];
+    const PreOutBufs& ob = pv.out[b];
+    PreOut o;
+    bool vis;
+    if (b == 0) {
+      o = o0;
+      vis = vis0;
+    } else {
+      o.depth = 0.f;
+      vis = preprocess_core<RAW, false>(v, g, i, in, o);
+    }
+    ob.tiles[i] = 0u;
+    ob.depth_key[i] = o.depth > 0.2f ? __float_as_uint(o.depth) : 0xFFFFFFFFu;
+    if (!vis) continue;
+    preprocess_color(v, g, i, in, o);
+    float4* rec = ob.rec + RECS * i;
+    rec[0] = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
+    rec[1] = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
+    rec[2] = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.tq);
+    ob.tiles[i] = (uint32_t)((o.rmax_x - o.rmin_x) * (o.rmax_y - o.rmin_y));
+    const uint2 rc = make_uint2((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16), (uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16));
+    ob.rect[i] = rc;
+    rec[3] = make_float4(__uint_as_float(rc.x), __uint_as_float(rc.y), 0.f, 0.f);
+    ob.clampw[i] = o.clamped;
+  }
+}
+
+// whether k_preprocess_views applies: raw GaussianModel leaves with the SH rest as its contiguous 16-B aligned leaf
+// (otherwise launch_preprocess_views runs launch_preprocess per view)
+static bool views_pass_ok(const GaussK& g) {
+  return g.raw && !g.colors && !g.cov3D && g.rest && g.M > 1 && g.rest_stride == 3 * (g.M - 1) &&
+         ((uintptr_t)g.rest & 15u) == 0;
+}
+
+int launch_preprocess_views(const PreViewsK& pv, const GaussK& g, const GeomBufs* gbs, hipStream_t s) {
+  if (g.P == 0 || pv.n == 0) return GSLM_OK;
+  if (!views_pass_ok(g)) {
+    for (int b = 0; b < pv.n; ++b) {
+      const int st = launch_preprocess(pv.v[b], g, gbs[b], nullptr, s);
+      if (st) return st;
+    }
+    return GSLM_OK;
+  }
+  const size_t lds = (size_t)256 * g.rest_stride * sizeof(float);
+  hipLaunchKernelGGL(k_preprocess_views<true>, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, pv, g);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 // One block per 256 consecutive Gaussians of the depth order: their (tile, id) pairs are one contiguous
 // output range, written by the whole block in element order (coalesced, and a large Gaussian's tiles are
 // spread over the block instead of one thread's loop).  Element e belongs to the last Gaussian whose
@@ -351,13 +439,15 @@ __global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint
 // k_duplicate over the union rects (the same emission: one block per 256 Gaussians of the depth order, elements in
 // order, a Gaussian's rect row-major), the point-list quadrant bits 0xF, and amask[e] = bits 4a..4a+3 the quadrant
 // mask of set a.  Each set's record of the block's Gaussians is staged in LDS once ([x y a b], [c tq rect]: 32 B,
-// rect 0 when the set culls it) and the masks are evaluated per element.  Dynamic LDS: n * 256 * 32 B.
+// rect 0 when the set culls it) -- all NS sets' loads issued together, then one wait -- and the masks are evaluated
+// per element.  Dynamic LDS: NS * 256 * 32 B.
+template <int NS>
 __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                           const uint32_t* __restrict__ offsets, uint32_t N,
                                                           const uint2* __restrict__ urect, UnionSets u,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                           uint32_t* __restrict__ amask) {
-  extern __shared__ float4 s_set[];  // [n][2][256]
+  extern __shared__ float4 s_set[];  // [NS][2][256]
   __shared__ uint32_t s_off[257];
   __shared__ uint32_t s_g[256];
   __shared__ uint32_t s_rc[256][3];  // x0, y0, width of the union rect
@@ -378,16 +468,24 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
       s_rc[tid][1] = (uint32_t)y0;
       s_rc[tid][2] = (uint32_t)(x1 - x0);
       s_g[tid] = g;
-      for (int a = 0; a < u.n; ++a) {
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-        if (u.tiles[a][g] != 0u) {
-          const float4* r = u.rec[a] + RECS * (size_t)g;
-          const float4 r3 = r[3];
-          r0 = r[0];
-          r1 = make_float4(r[1].x, r[2].w, r3.x, r3.y);
-        }
-        s_set[(2 * a) * 256 + tid] = r0;
-        s_set[(2 * a + 1) * 256 + tid] = r1;
+      uint32_t t[NS];
+      float4 r0[NS], r3[NS];
+      float r1x[NS], r2w[NS];
+#pragma unroll
+      for (int a = 0; a < NS; ++a) {  // every set's loads in flight together (a culled set's record is stale: masked)
+        const float4* r = u.rec[a] + RECS * (size_t)g;
+        t[a] = u.tiles[a][g];
+        r0[a] = r[0];
+        r1x[a] = r[1].x;
+        r2w[a] = r[2].w;
+        r3[a] = r[3];
+      }
+#pragma unroll
+      for (int a = 0; a < NS; ++a) {
+        const bool vis = t[a] != 0u;
+        s_set[(2 * a) * 256 + tid] = vis ? r0[a] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s_set[(2 * a + 1) * 256 + tid] = vis ? make_float4(r1x[a], r2w[a], r3[a].x, r3[a].y)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   } else {
@@ -405,7 +503,8 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
     const uint32_t dy = li / w;
     const int tx = (int)(s_rc[lo][0] + (li - dy * w)), ty = (int)(s_rc[lo][1] + dy);
     uint32_t m = 0u;
-    for (int a = 0; a < u.n; ++a) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
       const float4 r0 = s_set[(2 * a) * 256 + lo], r1 = s_set[(2 * a + 1) * 256 + lo];
       const uint32_t rlo = __float_as_uint(r1.z), rhi = __float_as_uint(r1.w);
       if (tx < (int)(rlo & 0xFFFFu) || ty < (int)(rlo >> 16) || tx >= (int)(rhi & 0xFFFFu) || ty >= (int)(rhi >> 16))
@@ -431,8 +530,20 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0 && N > 0) {
     const size_t lds = (size_t)u.n * 2 * 256 * sizeof(float4);
-    hipLaunchKernelGGL(k_duplicate_union, dim3((unsigned)((P + 255) / 256)), dim3(256), lds, s, P, v.gx, ug.sorted_idx,
-                       ug.offsets, (uint32_t)N, ug.rect, u, bb.keys0, bb.vals0, um.m0);
+    const dim3 grid((unsigned)((P + 255) / 256));
+    switch (u.n) {
+#define GSLM_DUP_UNION(NS)                                                                                         \
+  case NS:                                                                                                         \
+    hipLaunchKernelGGL(k_duplicate_union<NS>, grid, dim3(256), lds, s, P, v.gx, ug.sorted_idx, ug.offsets, (uint32_t)N, \
+                       ug.rect, u, bb.keys0, bb.vals0, um.m0);                                                      \
+    break;
+      GSLM_DUP_UNION(1) GSLM_DUP_UNION(2) GSLM_DUP_UNION(3) GSLM_DUP_UNION(4)
+      GSLM_DUP_UNION(5) GSLM_DUP_UNION(6) GSLM_DUP_UNION(7) GSLM_DUP_UNION(8)
+#undef GSLM_DUP_UNION
+      default:
+        set_error("union binning: 1..8 parameter sets");
+        return GSLM_ERR_INVALID;
+    }
     GSLM_LAUNCH_CHECK();
     bool alt = false;
     int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s, false, nullptr,

@@ -437,6 +437,22 @@ size_t img_layout(int H, int W, void* base, ImgBufs* out);
 size_t scratch_layout(int64_t P, int64_t N, void* base, ScratchBufs* out);
 
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s);
+// several views in one pass over the Gaussians (gslm_preprocess_views): each view's records, depth keys, tile counts,
+// rects and clamp words, no sort and no scan
+constexpr int MAX_PRE_VIEWS = 8;
+struct PreOutBufs {
+  float4* rec;
+  uint32_t* depth_key;
+  uint32_t* tiles;
+  uint2* rect;
+  uint32_t* clampw;
+};
+struct PreViewsK {
+  ViewK v[MAX_PRE_VIEWS];
+  PreOutBufs out[MAX_PRE_VIEWS];
+  int n;
+};
+int launch_preprocess_views(const PreViewsK& pv, const GaussK& g, const GeomBufs* gbs, hipStream_t s);
 // device_count: N is the list capacity and the count stays on the device (gslm_rasterize_dev); n_out (device, or
 // NULL) receives the count
 int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs& bb, int64_t N, hipStream_t s,

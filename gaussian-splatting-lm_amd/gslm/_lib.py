@@ -91,6 +91,8 @@ EXPORTS = {
     "gslm_preprocess_ordered": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians),
                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_int32, ctypes.c_void_p]),
+    "gslm_preprocess_views": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_void_p]),
     "gslm_num_rendered_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
@@ -267,9 +269,28 @@ def stream_handle(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+# Host copies of settings tensors (viewmatrix, projmatrix, campos, bg): a device tensor costs a device-to-host copy and
+# a stream synchronisation per read, and the drop-in Function reads the settings in its forward, backward and jvp.  A
+# camera's matrices are the same tensors call after call, so the copy is cached per tensor object, valid while the
+# tensor lives at the same version (any in-place write bumps it).
+_HOST_CACHE = {}
+
+
 def _host_floats(t, n):
     if isinstance(t, torch.Tensor):
-        return [float(x) for x in t.detach().reshape(-1).to("cpu", torch.float32).tolist()][:n]
+        hit = _HOST_CACHE.get(id(t))
+        if hit is not None and hit[0]() is t and hit[1] == t._version and hit[2] == n:
+            return hit[3]
+        vals = [float(x) for x in t.detach().reshape(-1).to("cpu", torch.float32).tolist()][:n]
+        if t.is_cuda:
+            import weakref
+            key = id(t)
+            try:
+                ref = weakref.ref(t, lambda _r, key=key: _HOST_CACHE.pop(key, None))
+            except TypeError:
+                return vals
+            _HOST_CACHE[key] = (ref, t._version, n, vals)
+        return vals
     return [float(x) for x in list(t)][:n]
 
 

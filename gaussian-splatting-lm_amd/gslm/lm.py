@@ -816,7 +816,8 @@ class LossEvaluator:
         self._order_key, self._orders = None, [None] * len(cams)
         # the shared binning of evaluate_points (gslm_union_*): per batch position k its sets' geometries, the union
         # geometry and the union list
-        self.uslots = [dict(geoms=[], ugeom=None, binning=None) for _ in range(self.batch)]
+        self.uslots = [[dict(geoms=[], ugeom=None) for _ in range(self.batch)] for _ in range(2)]
+        self.ubins = [None] * self.batch
         self.union_counts = []
 
     def _slot(self, k, P):
@@ -946,8 +947,10 @@ class LossEvaluator:
         return loss
 
     # ---- the line search's six points with one binning per view (include/gslm.h "shared binning", ABI 8) ----
-    def _ugeom(self, k, n, P):
-        sl = self.uslots[k]
+    def _uslot(self, par, k, n, P):
+        """Batch position k's geometries (n sets) and union geometry, of slot set `par` (two sets alternate over the
+        batches: a batch's preprocesses overwrite the slots of the batch before the previous one)."""
+        sl = self.uslots[par][k]
         nb = lib.gslm_geom_bytes(P)
         while len(sl["geoms"]) < n:
             sl["geoms"].append(None)
@@ -961,10 +964,13 @@ class LossEvaluator:
     def evaluate_points(self, sets):
         """The validation loss at each of n <= 8 parameter sets (snapshots sharing the model's frozen xyz: the six
         line-search points of train_jvp.py:262-277, param_snapshot), as a list of device doubles -- each bitwise equal
-        to evaluate() with the model at that set.  Per view: the n preprocesses (one depth order), ONE binning over the
-        union of the sets' rects (gslm_union_geometry / gslm_union_binning: 4 mask bits per set and list entry, carried
-        through the tile sort), then the n blends + losses through it (gslm_rasterize_loss_slot).  union_counts[i]:
-        view i's union list length (the last call)."""
+        to evaluate() with the model at that set.  Per view: the n sets' per-Gaussian stage (gslm_preprocess_views: one
+        pass over the Gaussians per set for the batch's views), ONE binning over the union of the sets' rects
+        (gslm_union_geometry / gslm_union_binning: 4 mask bits per set and list entry, carried through the tile sort),
+        then the n blends + losses through it (gslm_rasterize_loss_slot).
+        Pipelining: a batch's preprocesses, union geometries and pair-count read-back run on the main stream while the
+        previous batch's binnings and blends run on the side streams (two alternating slot sets), so the read-back does
+        not drain the device.  union_counts[i]: view i's union list length (the last call)."""
         n = len(sets)
         if not 1 <= n <= 8:
             raise ValueError("evaluate_points takes 1..8 parameter sets")
@@ -981,44 +987,56 @@ class LossEvaluator:
             self._order_key, self._orders = key, [None] * V
         losses = [torch.zeros(max(V, 1), dtype=torch.float64, device=self.device) for _ in range(n)]
         self.union_counts = [0] * V
-        for st in self.streams:
-            if st is not None:
-                st.wait_stream(main)
-        for b0 in range(0, V, self.batch):
+        side = [st for st in self.streams if st is not None]
+        done = [None, None]  # per slot set: events after the side streams' last use of its slots
+        for bi, b0 in enumerate(range(0, V, self.batch)):
+            par = bi & 1
             idx = list(range(b0, min(V, b0 + self.batch)))
-            slots = [self._ugeom(k, n, P) for k in range(len(idx))]
-            for k, (sl, i) in enumerate(zip(slots, idx)):
-                vw = self.views[i]
-                _, sh = self._stream(k)
-                mode0 = 2
-                if self._orders[i] is None:
-                    self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
-                    mode0 = 1
-                for a in range(n):
-                    check(lib.gslm_preprocess_ordered(ctypes.byref(vw), ctypes.byref(gs[a]), sl["geoms"][a].data_ptr(),
-                                                      sl["geoms"][a].numel(), None, self._orders[i].data_ptr(),
-                                                      mode0 if a == 0 else 2, sh), "gslm_preprocess_ordered")
-                ge = (ctypes.c_void_p * n)(*[sl["geoms"][a].data_ptr() for a in range(n)])
-                check(lib.gslm_union_geometry(ctypes.byref(vw), P, ge, n, self._orders[i].data_ptr(),
-                                              sl["ugeom"].data_ptr(), sl["ugeom"].numel(), sh), "gslm_union_geometry")
-            for st in self.streams:
-                if st is not None:
-                    main.wait_stream(st)
+            if done[par] is not None:  # the batch before the previous one has finished with these slots
+                for ev in done[par]:
+                    main.wait_event(ev)
+            slots = [self._uslot(par, k, n, P) for k in range(len(idx))]
+            # 1. the sets' per-Gaussian stage (main stream); a view without its depth order sorts it with set 0
+            fresh = [k for k, i in enumerate(idx) if self._orders[i] is None]
+            for k in fresh:
+                i = idx[k]
+                self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(gs[0]),
+                                                  slots[k]["geoms"][0].data_ptr(), slots[k]["geoms"][0].numel(), None,
+                                                  self._orders[i].data_ptr(), 1, main_h), "gslm_preprocess_ordered")
+            for a in range(n):
+                ks = [k for k in range(len(idx)) if not (a == 0 and k in fresh)]
+                if not ks:
+                    continue
+                vws = (_lib.GslmView * len(ks))(*[self.views[idx[k]] for k in ks])
+                ge = (ctypes.c_void_p * len(ks))(*[slots[k]["geoms"][a].data_ptr() for k in ks])
+                check(lib.gslm_preprocess_views(vws, len(ks), ctypes.byref(gs[a]), ge, slots[ks[0]]["geoms"][a].numel(),
+                                                main_h), "gslm_preprocess_views")
+            # 2. union geometries and their pair counts (main stream; the read-back waits for main only)
+            for k, i in enumerate(idx):
+                ge = (ctypes.c_void_p * n)(*[slots[k]["geoms"][a].data_ptr() for a in range(n)])
+                check(lib.gslm_union_geometry(ctypes.byref(self.views[i]), P, ge, n, self._orders[i].data_ptr(),
+                                              slots[k]["ugeom"].data_ptr(), slots[k]["ugeom"].numel(), main_h),
+                      "gslm_union_geometry")
             ugeoms = (ctypes.c_void_p * len(idx))(*[sl["ugeom"].data_ptr() for sl in slots])
             Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
             Ns = (ctypes.c_int64 * len(idx))()
-            check(lib.gslm_num_rendered_many(ugeoms, Ps, len(idx), Ns, main_h), "gslm_num_rendered_many")  # syncs
+            check(lib.gslm_num_rendered_many(ugeoms, Ps, len(idx), Ns, main_h), "gslm_num_rendered_many")
+            # 3. binning + the n blends of each view on its side stream
+            for st in side:
+                st.wait_stream(main)
             for k, (sl, i) in enumerate(zip(slots, idx)):
                 vw = self.views[i]
                 H, W, N = vw.image_height, vw.image_width, int(Ns[k])
                 self.union_counts[i] = N
                 st, sh = self._stream(k)
                 need = lib.gslm_union_binning_bytes(N, H, W)
-                if sl["binning"] is None or sl["binning"].numel() < need:
-                    if sl["binning"] is not None and st is not None:
+                bins = self.ubins
+                if bins[k] is None or bins[k].numel() < need:
+                    if bins[k] is not None and st is not None:
                         main.wait_stream(st)  # freed on the main stream: after its last use
-                    sl["binning"] = _lib.u8(int(need * 1.25) + 4096, self.device)
-                binning = sl["binning"]
+                    bins[k] = _lib.u8(int(need * 1.25) + 4096, self.device)
+                binning = bins[k]
                 ge = (ctypes.c_void_p * n)(*[sl["geoms"][a].data_ptr() for a in range(n)])
                 check(lib.gslm_union_binning(ctypes.byref(vw), P, sl["ugeom"].data_ptr(), binning.data_ptr(),
                                              binning.numel(), N, ge, n, sh), "gslm_union_binning")
@@ -1030,9 +1048,15 @@ class LossEvaluator:
                                                        None if m is None else m.data_ptr(), scr.data_ptr(),
                                                        scr.numel() * 8, losses[a].data_ptr() + 8 * i, 0, sh),
                           "gslm_rasterize_loss_slot")
-        for st in self.streams:
-            if st is not None:
-                main.wait_stream(st)
+            if side:
+                evs = []
+                for st in side:
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    evs.append(ev)
+                done[par] = evs
+        for st in side:
+            main.wait_stream(st)
         out = []
         for a in range(n):
             loss = losses[a][:V].sum() if V else losses[a][0]
@@ -1070,6 +1094,9 @@ def update_params(model, layout, step, scale, skip_xyz=False):
         model._rotation.add_(v["rotation"], alpha=scale)
         model._opacity.add_(v["opacity"], alpha=scale)
         model._exposure.add_(v["exposure"], alpha=scale)
+
+
+_VAL_CACHE = {}  # lm_step's last validation evaluator: {"last": (key, evaluator)}
 
 
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
@@ -1137,8 +1164,21 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     lap("cg_ms")
     full = ParamLayout(model._xyz.shape[0], 1 + model._features_rest.shape[1], model._exposure.shape[0])
     mine_val = [val_cams[i] for i in shard_views(len(val_cams), rank, n)] if sharded else val_cams
-    val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
-                        reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
+    # the validation evaluator (its workspaces and the views' cached depth orders) is kept from one LM step to the
+    # next while the model, the validation cameras (held by it, so their ids stay theirs) and the settings are the same
+    imgs = [(getattr(c, "original_image", None), getattr(c, "alpha_mask", None)) for c in mine_val]
+    vkey = (id(model), model.active_sh_degree, tuple(id(c) for c in mine_val), tuple(id(t) for p in imgs for t in p),
+            str(device), val_batch, evaluator_cls, sharded, id(group),
+            tuple(float(x) for x in torch.as_tensor(bg).reshape(-1).tolist()))
+    hit = _VAL_CACHE.get("last")
+    if hit is not None and hit[0] == vkey:
+        val = hit[1]
+    else:
+        _VAL_CACHE.pop("last", None)
+        val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
+                            reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
+        val.held = (model, list(mine_val), imgs)
+        _VAL_CACHE["last"] = (vkey, val)
     val_start = float(val.evaluate()) if val_at_start else None
     if val_at_start:
         lap("val_start_ms")

@@ -119,6 +119,12 @@ int gslm_preprocess(const gslm_view* view, const gslm_gaussians* g, void* geom, 
  *      train_jvp.py:221-227,262-279: the same point list, bitwise, without the four depth-sort passes). */
 int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* g, void* geom, size_t geom_bytes,
                             int32_t* out_radii, uint32_t* depth_order, int32_t order_mode, void* stream);
+/* The per-Gaussian stage of gslm_preprocess for nviews <= 8 views in one pass over the Gaussians (ABI 8): each view's
+ * render records, depth keys, tile counts and rects into geoms[b] (each >= gslm_geom_bytes(P)), bitwise as
+ * gslm_preprocess writes them, with no depth sort and no tile-count scan (the line search's parameter sets:
+ * gslm_union_geometry consumes only those).  A Gaussian's 236 B of inputs (SH 3) are read once for the views. */
+int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, void* const* geoms,
+                          size_t geom_bytes, void* stream);
 /* Synchronous read of the number of (tile, Gaussian) pairs produced by gslm_preprocess. */
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out_num_rendered, void* stream);
 /* The same for n preprocessed geometries (geoms[k] over Ps[k] Gaussians) with ONE stream synchronisation:
@@ -163,7 +169,8 @@ int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* str
  * point, and each point's exact point list is the subsequence of one list binned over the union of the points' rects:
  * the entries whose tile lies in that point's rect, in the same (tile, depth, index) order.  So a view is binned once
  * for the six points instead of once per point (gslm.lm.LossEvaluator.evaluate_points):
- *   1. gslm_preprocess_ordered of each point's parameters into its own geometry workspace (geoms[a], one depth order);
+ *   1. each point's per-Gaussian stage into its own geometry workspace (geoms[a]: gslm_preprocess_views, or
+ *      gslm_preprocess_ordered, which also writes the view's depth order);
  *   2. gslm_union_geometry: the union of the n <= 8 points' rects per Gaussian into union_geom, its tile counts scanned
  *      in depth order -- gslm_num_rendered(union_geom) is the union list's length N;
  *   3. gslm_union_binning (workspace >= gslm_union_binning_bytes(N, H, W)): duplicate + tile sort + ranges of the union

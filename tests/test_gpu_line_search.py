@@ -152,3 +152,54 @@ def test_union_lm_step_matches_reference_golden():
     assert np.abs(losses - ref).max() <= 1e-4 * ref.max()
     fin = float(L["ten_final_val_loss"])
     assert abs(out["final_val_loss"] - fin) <= 1e-4 * fin
+
+
+@pytest.mark.parametrize("nviews", [1, 3, 8])
+def test_preprocess_views_equals_per_view_preprocess(nviews):
+    """gslm_preprocess_views (one pass over the Gaussians for several views) writes each view's records, tile counts
+    and rects bitwise as gslm_preprocess does (ragged P, mixed image sizes)."""
+    import ctypes
+    from gslm import _lib
+    from gslm.cameras import orbit_cameras
+    from gslm.model import synthetic_gaussians
+    from gslm.params import raw_gaussians
+    lib = _lib.lib
+    m = synthetic_gaussians(10_007, 3, seed=1, s0=0.02).to("cuda")
+    g = raw_gaussians(m)
+    cams = orbit_cameras(nviews, 96, 80, seed=3)
+    if nviews > 1:
+        cams[1] = orbit_cameras(2, 130, 57, seed=9)[1]
+    views = (_lib.GslmView * nviews)(*[_lib.view_from_camera(c, torch.zeros(3), 3) for c in cams])
+    nb = lib.gslm_geom_bytes(g.P)
+    a = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(nviews)]
+    b = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(nviews)]
+    for k in range(nviews):
+        assert lib.gslm_preprocess(ctypes.byref(views[k]), ctypes.byref(g), a[k].data_ptr(), nb, None, None) == 0
+    ge = (ctypes.c_void_p * nviews)(*[t.data_ptr() for t in b])
+    assert lib.gslm_preprocess_views(views, nviews, ctypes.byref(g), ge, nb, None) == 0, lib.gslm_last_error()
+    torch.cuda.synchronize()
+    P = g.P
+    rec = 64 * P  # render records [P][4] float4
+    keys = 4 * P
+    for k in range(nviews):
+        ra, rb = a[k][:rec].view(torch.float32).view(P, 16), b[k][:rec].view(torch.float32).view(P, 16)
+        tiles_a = a[k][_off(rec, keys):_off(rec, keys) + keys].view(torch.int32)
+        tiles_b = b[k][_off(rec, keys):_off(rec, keys) + keys].view(torch.int32)
+        assert torch.equal(tiles_a, tiles_b)
+        vis = tiles_a > 0
+        assert int(vis.sum()) > 0
+        assert torch.equal(ra[vis].view(torch.int32), rb[vis].view(torch.int32))
+        # rects (the depth keys are not comparable: gslm_preprocess's depth sort reuses their buffer)
+        r0 = _off(rec, keys) + _al(keys)
+        rect_a = a[k][r0:r0 + 8 * P].view(torch.int64)
+        rect_b = b[k][r0:r0 + 8 * P].view(torch.int64)
+        assert torch.equal(rect_a[vis], rect_b[vis])
+
+
+def _al(x):
+    return (x + 255) // 256 * 256
+
+
+def _off(rec, keys):
+    """Byte offset of the tile counts in the geometry layout (rec, depth_key, tiles, ...; 256-B aligned, api.hip)."""
+    return _al(rec) + _al(keys)

@@ -63,7 +63,7 @@ def _cholesky_ref(B):
             r = G[:, j, b] - np.einsum("pq,pq->p", R[:, :j, j], R[:, :j, b])
             R[:, j, b] = np.where(keep, r / np.where(keep, R[:, j, j], 1.0), 0.0)
             d -= R[:, j, b] ** 2
-        R[:, b, b] = np.where((G[:, b, b] > 0) & (d > 1e-12 * G[:, b, b]), np.sqrt(np.maximum(d, 0)), 0.0)
+        R[:, b, b] = np.where((G[:, b, b] > 0) & (d > 1e-7 * G[:, b, b]), np.sqrt(np.maximum(d, 0)), 0.0)
     return np.concatenate([R[:, :b + 1, b] for b in range(V)], axis=1)
 
 
@@ -123,3 +123,41 @@ def test_rest_coords_projection_and_roundtrip():
     back = _coords(views, V, g, R, 0, _coords(views, V, g, R, 1, ts, P), P)
     torch.cuda.synchronize()
     assert (back - ts).abs().max() <= 1e-5 * ts.abs().max()
+
+
+def test_nearly_collinear_views_expand_consistently():
+    """Views whose SH-rest directions are nearly parallel (a camera moved by 1e-4 .. 1e-2 of the orbit radius): the
+    expansion of coordinates c is what the CG kernels assume it is -- B_b^T expand(c) = (R^T c)_b for every view b
+    (view b's colour tangent from the coordinates) -- to 1e-3 of |B| |c|, kept views and dropped ones alike (the float
+    R's rounding is amplified by 1 / R[b][b], which the drop cut bounds)."""
+    from gslm import _lib
+    from gslm.cameras import Camera, orbit_cameras
+    from gslm.model import synthetic_gaussians
+    from gslm.params import raw_gaussians
+    base = orbit_cameras(3, W, H, seed=2)
+    cams = list(base)
+    for k, eps in enumerate((1e-4, 1e-3, 1e-2)):
+        c0 = base[k]
+        # the same camera translated along its own x axis by eps of the orbit radius (3)
+        T_ = np.asarray(c0.T, dtype=np.float64) + np.array([3.0 * eps, 0.0, 0.0])
+        cams.append(Camera(np.asarray(c0.R), T_, c0.FoVx, c0.FoVy, width=W, height=H))
+    model = synthetic_gaussians(4000, 3, seed=0, s0=0.03, n_cams=len(cams)).to("cuda")
+    views = (_lib.GslmView * len(cams))()
+    for k, c in enumerate(cams):
+        views[k] = _lib.view_from_camera(c, torch.zeros(3), 3)
+    g = raw_gaussians(model)
+    P, V = model._xyz.shape[0], len(cams)
+    R = _rest_basis(views, V, g, P)
+    c = torch.randn(P, 3 * V, generator=torch.Generator().manual_seed(5)).cuda()
+    t = _coords(views, V, g, R, 0, c, P)
+    torch.cuda.synchronize()
+    B = torch.from_numpy(_basis(model, cams))                       # [V, P, 15]
+    lhs = torch.einsum("vpk,pkc->pvc", B, t.double().cpu().view(P, 15, 3))
+    Rp = R.double().cpu().view(P, -1)
+    rhs = torch.zeros(P, V, 3, dtype=torch.float64)
+    cc = c.double().cpu().view(P, V, 3)
+    for b in range(V):
+        for j in range(b + 1):
+            rhs[:, b] += Rp[:, b * (b + 1) // 2 + j, None] * cc[:, j]
+    scale = B.norm(dim=2).max() * cc.norm(dim=(1, 2)).max()
+    assert ((lhs - rhs).abs().max() / scale).item() <= 1e-3
