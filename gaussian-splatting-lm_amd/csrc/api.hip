@@ -246,7 +246,7 @@ int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* gi, voi
 }
 
 int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* gi, void* const* geoms,
-                          size_t geom_bytes, void* stream) {
+                          size_t geom_bytes, const uint32_t* const* depth_pos, void* stream) {
   if (!views || !gi || !geoms || nviews < 1 || nviews > MAX_PRE_VIEWS) {
     set_error("preprocess_views: NULL argument or nviews outside 1..8");
     return GSLM_ERR_INVALID;
@@ -260,10 +260,20 @@ int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gau
     if ((st = make_gauss(gi, &pv.v[b], &g, false))) return st;  // each view's SH degree against the stored coefficients
     if (geom_bytes < gslm_geom_bytes(g.P) || (!geoms[b] && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
     geom_layout(g.P, geoms[b], &gbs[b]);
-    pv.out[b] = PreOutBufs{gbs[b].rec, gbs[b].depth_key, gbs[b].tiles, gbs[b].rect, gbs[b].clampw};
+    const uint32_t* pos = depth_pos ? depth_pos[b] : nullptr;
+    if (depth_pos && !pos && g.P) { set_error("preprocess_views: NULL depth positions"); return GSLM_ERR_INVALID; }
+    pv.out[b] = PreOutBufs{gbs[b].rec, gbs[b].depth_key, gbs[b].tiles, gbs[b].rect, gbs[b].clampw, pos};
   }
   pv.n = nviews;
   return launch_preprocess_views(pv, g, gbs, (hipStream_t)stream);
+}
+
+int gslm_depth_positions(const uint32_t* depth_order, int64_t P, uint32_t* depth_pos, void* stream) {
+  if (P < 0 || P > MAX_P || (P && (!depth_order || !depth_pos))) {
+    set_error("depth_positions: NULL order / positions or P out of range");
+    return GSLM_ERR_INVALID;
+  }
+  return launch_depth_positions(P, depth_order, depth_pos, (hipStream_t)stream);
 }
 
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
@@ -402,14 +412,13 @@ size_t gslm_union_binning_bytes(int64_t N, int32_t H, int32_t W) {
   return union_masks_layout(N, ntiles, nullptr, nullptr);
 }
 
-int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n,
-                        const uint32_t* depth_order, void* union_geom, size_t union_geom_bytes, void* stream) {
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, void* union_geom,
+                        size_t union_geom_bytes, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
   if (P < 0 || P > MAX_P) { set_error("P out of range [0, 2^28 - 1]"); return GSLM_ERR_INVALID; }
   if (union_geom_bytes < gslm_geom_bytes(P) || (!union_geom && P)) { set_error("union geometry workspace too small"); return GSLM_ERR_CAPACITY; }
-  if (P && !depth_order) { set_error("union_geometry: NULL depth_order"); return GSLM_ERR_INVALID; }
   UnionSets u;
   if ((st = union_sets(geoms, n, P, &u))) return st;
   GeomBufs ug;
@@ -420,9 +429,8 @@ int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geo
     return GSLM_OK;
   }
   if ((st = launch_union_rect(P, u, ug, s))) return st;
-  GSLM_HIP_CHECK(hipMemcpyAsync(ug.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
-  // the union tile counts in depth order: k_duplicate_union's offsets, and the pair count in counters[0]
-  return exclusive_scan_u32(ug.tiles, ug.sorted_idx, ug.offsets, P, ug.scan_tmp, ug.counters, s);
+  // the union tile counts, already in depth order: k_duplicate_union's offsets, and the pair count in counters[0]
+  return exclusive_scan_u32(ug.tiles, nullptr, ug.offsets, P, ug.scan_tmp, ug.counters, s);
 }
 
 int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,

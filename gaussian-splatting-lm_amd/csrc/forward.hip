@@ -188,6 +188,22 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PreViewsK pv, GaussK g
       o.depth = 0.f;
       vis = preprocess_core<RAW, false>(v, g, i, in, o);
     }
+    if (ob.pos) {
+      // depth space (the line search's union lists): the render record alone, at the Gaussian's depth position, its
+      // rect slot zero when culled -- one 64-B record per Gaussian, read in depth order by the union binning
+      float4* rec = ob.rec + RECS * (size_t)ob.pos[i];
+      if (vis) {
+        preprocess_color(v, g, i, in, o);
+        rec[0] = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
+        rec[1] = make_float4(o.conic[2], o.opac, o.rgb[0], o.rgb[1]);
+        rec[2] = make_float4(o.rgb[2], 1.0f / o.depth, __uint_as_float(o.clamped), o.tq);
+        rec[3] = make_float4(__uint_as_float((uint32_t)o.rmin_x | ((uint32_t)o.rmin_y << 16)),
+                             __uint_as_float((uint32_t)o.rmax_x | ((uint32_t)o.rmax_y << 16)), 0.f, 0.f);
+      } else {
+        rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      continue;
+    }
     ob.tiles[i] = 0u;
     ob.depth_key[i] = o.depth > 0.2f ? __float_as_uint(o.depth) : 0xFFFFFFFFu;
     if (!vis) continue;
@@ -416,7 +432,18 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
 // elsewhere; the tile sort carries them with the pairs.  A blend that visits by those bits visits the exact list's
 // entries, in its order, with the same records: the same image and loss, bitwise (gslm_rasterize_loss_slot).
 
-// per Gaussian: the union of the rects of the sets where it is visible (tiles > 0), as the union geometry's tile
+// The union list is built in DEPTH SPACE: the sets' records sit at their Gaussians' depth positions s (gslm_preprocess_
+// views with depth positions), so every pass below reads them coalesced in s and the point list's values are depth
+// positions.  The blend indexes the set's records by them (the same records, the same (tile, depth, index) order).
+
+// k_depth_positions: pos[order[s]] = s (the depth order's inverse)
+__global__ __launch_bounds__(256) void k_depth_positions(int64_t P, const uint32_t* __restrict__ order,
+                                                          uint32_t* __restrict__ pos) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < P) pos[order[s]] = (uint32_t)s;
+}
+
+// per depth position: the union of the sets' rects (a culled set's rect slot is zero), as the union geometry's tile
 // count and rect
 __global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint32_t* __restrict__ utiles,
                                                      uint2* __restrict__ urect) {
@@ -424,32 +451,31 @@ __global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint
   if (i >= P) return;
   uint32_t x0 = 0xFFFFu, y0 = 0xFFFFu, x1 = 0u, y1 = 0u;
   for (int a = 0; a < u.n; ++a) {
-    if (u.tiles[a][i] == 0u) continue;
-    const uint2 rc = u.rect[a][i];
-    x0 = min(x0, rc.x & 0xFFFFu);
-    y0 = min(y0, rc.x >> 16);
-    x1 = max(x1, rc.y & 0xFFFFu);
-    y1 = max(y1, rc.y >> 16);
+    const float4 r3 = u.rec[a][RECS * i + 3];
+    const uint32_t lo = __float_as_uint(r3.x), hi = __float_as_uint(r3.y);
+    if (hi == 0u) continue;  // culled in set a
+    x0 = min(x0, lo & 0xFFFFu);
+    y0 = min(y0, lo >> 16);
+    x1 = max(x1, hi & 0xFFFFu);
+    y1 = max(y1, hi >> 16);
   }
   const bool any = x1 > x0 && y1 > y0;
   utiles[i] = any ? (x1 - x0) * (y1 - y0) : 0u;
   urect[i] = any ? make_uint2(x0 | (y0 << 16), x1 | (y1 << 16)) : make_uint2(0u, 0u);
 }
 
-// k_duplicate over the union rects (the same emission: one block per 256 Gaussians of the depth order, elements in
-// order, a Gaussian's rect row-major), the point-list quadrant bits 0xF, and amask[e] = bits 4a..4a+3 the quadrant
-// mask of set a.  Each set's record of the block's Gaussians is staged in LDS once ([x y a b], [c tq rect]: 32 B,
-// rect 0 when the set culls it) -- all NS sets' loads issued together, then one wait -- and the masks are evaluated
-// per element.  Dynamic LDS: NS * 256 * 32 B.
+// k_duplicate over the union rects in depth space (the same emission as k_duplicate: one block per 256 depth
+// positions, elements in order, a Gaussian's rect row-major), the value the depth position with quadrant bits 0xF,
+// and amask[e] = bits 4a..4a+3 the quadrant mask of set a.  Each set's record of the block's Gaussians (coalesced in
+// depth space) is staged in LDS once ([x y a b], [c tq rect]: 32 B) and the masks are evaluated per element.
+// Dynamic LDS: NS * 256 * 32 B.
 template <int NS>
-__global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
-                                                          const uint32_t* __restrict__ offsets, uint32_t N,
-                                                          const uint2* __restrict__ urect, UnionSets u,
+__global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ offsets,
+                                                          uint32_t N, const uint2* __restrict__ urect, UnionSets u,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                           uint32_t* __restrict__ amask) {
   extern __shared__ float4 s_set[];  // [NS][2][256]
   __shared__ uint32_t s_off[257];
-  __shared__ uint32_t s_g[256];
   __shared__ uint32_t s_rc[256][3];  // x0, y0, width of the union rect
   const int tid = threadIdx.x;
   const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
@@ -457,35 +483,29 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
   const uint32_t base = offsets[s0];
   uint32_t n = 0;
   if (s < P) {
-    const uint32_t g = sorted_idx[s];
     const uint32_t o = offsets[s];
     n = (s + 1 < P ? offsets[s + 1] : N) - o;
     s_off[tid] = o - base;
     if (n) {
-      const uint2 rc = urect[g];
+      const uint2 rc = urect[s];
       const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
       s_rc[tid][0] = (uint32_t)x0;
       s_rc[tid][1] = (uint32_t)y0;
       s_rc[tid][2] = (uint32_t)(x1 - x0);
-      s_g[tid] = g;
-      uint32_t t[NS];
       float4 r0[NS], r3[NS];
       float r1x[NS], r2w[NS];
 #pragma unroll
-      for (int a = 0; a < NS; ++a) {  // every set's loads in flight together (a culled set's record is stale: masked)
-        const float4* r = u.rec[a] + RECS * (size_t)g;
-        t[a] = u.tiles[a][g];
+      for (int a = 0; a < NS; ++a) {  // every set's loads in flight together
+        const float4* r = u.rec[a] + RECS * (size_t)s;
         r0[a] = r[0];
         r1x[a] = r[1].x;
         r2w[a] = r[2].w;
         r3[a] = r[3];
       }
 #pragma unroll
-      for (int a = 0; a < NS; ++a) {
-        const bool vis = t[a] != 0u;
-        s_set[(2 * a) * 256 + tid] = vis ? r0[a] : make_float4(0.f, 0.f, 0.f, 0.f);
-        s_set[(2 * a + 1) * 256 + tid] = vis ? make_float4(r1x[a], r2w[a], r3[a].x, r3[a].y)
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int a = 0; a < NS; ++a) {  // a culled set's record holds a zero rect (and stale values: no tile passes)
+        s_set[(2 * a) * 256 + tid] = r0[a];
+        s_set[(2 * a + 1) * 256 + tid] = make_float4(r1x[a], r2w[a], r3[a].x, r3[a].y);
       }
     }
   } else {
@@ -512,9 +532,16 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
       m |= quad_mask(quad_cull_prep(r0.x, r0.y, r0.z, r0.w, r1.x, r1.y), tx, ty) << (4 * a);
     }
     keys[base + e] = (uint32_t)(ty * gx + tx);
-    vals[base + e] = s_g[lo] | (0xFu << ID_BITS);
+    vals[base + e] = (uint32_t)(s0 + lo) | (0xFu << ID_BITS);
     amask[base + e] = m;
   }
+}
+
+int launch_depth_positions(int64_t P, const uint32_t* order, uint32_t* pos, hipStream_t s) {
+  if (P <= 0) return GSLM_OK;
+  hipLaunchKernelGGL(k_depth_positions, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, order, pos);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
 }
 
 int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s) {
@@ -534,8 +561,8 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
     switch (u.n) {
 #define GSLM_DUP_UNION(NS)                                                                                         \
   case NS:                                                                                                         \
-    hipLaunchKernelGGL(k_duplicate_union<NS>, grid, dim3(256), lds, s, P, v.gx, ug.sorted_idx, ug.offsets, (uint32_t)N, \
-                       ug.rect, u, bb.keys0, bb.vals0, um.m0);                                                      \
+    hipLaunchKernelGGL(k_duplicate_union<NS>, grid, dim3(256), lds, s, P, v.gx, ug.offsets, (uint32_t)N, ug.rect, u, \
+                       bb.keys0, bb.vals0, um.m0);                                                                   \
     break;
       GSLM_DUP_UNION(1) GSLM_DUP_UNION(2) GSLM_DUP_UNION(3) GSLM_DUP_UNION(4)
       GSLM_DUP_UNION(5) GSLM_DUP_UNION(6) GSLM_DUP_UNION(7) GSLM_DUP_UNION(8)

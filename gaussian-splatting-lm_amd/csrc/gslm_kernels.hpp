@@ -446,6 +446,7 @@ struct PreOutBufs {
   uint32_t* tiles;
   uint2* rect;
   uint32_t* clampw;
+  const uint32_t* pos;  // or NULL: depth space (the render records alone, at pos[i]; rect slot zero when culled)
 };
 struct PreViewsK {
   ViewK v[MAX_PRE_VIEWS];
@@ -482,6 +483,7 @@ struct UnionMasks {
 };
 size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* out);
 int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s);
+int launch_depth_positions(int64_t P, const uint32_t* order, uint32_t* pos, hipStream_t s);
 int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,
                          int64_t N, const UnionSets& u, hipStream_t s);
 int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const ImgBufs& ib, float* out_color,

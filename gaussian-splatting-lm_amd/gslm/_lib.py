@@ -92,7 +92,9 @@ EXPORTS = {
                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_int32, ctypes.c_void_p]),
     "gslm_preprocess_views": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int32, ctypes.POINTER(GslmGaussians),
-                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_void_p]),
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "gslm_depth_positions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_num_rendered_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "gslm_rasterize": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
@@ -114,8 +116,7 @@ EXPORTS = {
     "gslm_num_rendered_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_union_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "gslm_union_geometry": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
-                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                           ctypes.c_void_p]),
+                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "gslm_union_binning": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.c_int32, ctypes.c_void_p]),

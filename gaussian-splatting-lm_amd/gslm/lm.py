@@ -814,6 +814,7 @@ class LossEvaluator:
         self.loss_scratch = [torch.empty(nb // 8 + 1, dtype=torch.float64, device=device) for _ in self.streams]
         self.num_rendered = [0] * len(cams)
         self._order_key, self._orders = None, [None] * len(cams)
+        self._pos = [None] * len(cams)  # the depth orders' inverses (gslm_depth_positions), for evaluate_points
         # the shared binning of evaluate_points (gslm_union_*): per batch position k its sets' geometries, the union
         # geometry and the union list
         self.uslots = [[dict(geoms=[], ugeom=None) for _ in range(self.batch)] for _ in range(2)]
@@ -865,6 +866,7 @@ class LossEvaluator:
         key = (xyz.data_ptr(), xyz._version, P)
         if key != self._order_key:  # xyz moved: sort again
             self._order_key, self._orders = key, [None] * V
+            self._pos = [None] * V
         # device-count renders' pair counts: allocated and zeroed on the main stream BEFORE the side streams wait on
         # it, so no stream's k_ranges count write can precede the zero fill
         counts = torch.zeros(max(V, 1), dtype=torch.int32, device=self.device)
@@ -964,10 +966,11 @@ class LossEvaluator:
     def evaluate_points(self, sets):
         """The validation loss at each of n <= 8 parameter sets (snapshots sharing the model's frozen xyz: the six
         line-search points of train_jvp.py:262-277, param_snapshot), as a list of device doubles -- each bitwise equal
-        to evaluate() with the model at that set.  Per view: the n sets' per-Gaussian stage (gslm_preprocess_views: one
-        pass over the Gaussians per set for the batch's views), ONE binning over the union of the sets' rects
-        (gslm_union_geometry / gslm_union_binning: 4 mask bits per set and list entry, carried through the tile sort),
-        then the n blends + losses through it (gslm_rasterize_loss_slot).
+        to evaluate() with the model at that set.  Per view: the n sets' render records in depth space
+        (gslm_preprocess_views with the view's depth positions: one pass over the Gaussians per set for the batch's
+        views), ONE binning over the union of the sets' rects (gslm_union_geometry / gslm_union_binning: 4 mask bits
+        per set and list entry, carried through the tile sort), then the n blends + losses through it
+        (gslm_rasterize_loss_slot).
         Pipelining: a batch's preprocesses, union geometries and pair-count read-back run on the main stream while the
         previous batch's binnings and blends run on the side streams (two alternating slot sets), so the read-back does
         not drain the device.  union_counts[i]: view i's union list length (the last call)."""
@@ -985,6 +988,7 @@ class LossEvaluator:
         key = (xyz.data_ptr(), xyz._version, P)
         if key != self._order_key:
             self._order_key, self._orders = key, [None] * V
+            self._pos = [None] * V
         losses = [torch.zeros(max(V, 1), dtype=torch.float64, device=self.device) for _ in range(n)]
         self.union_counts = [0] * V
         side = [st for st in self.streams if st is not None]
@@ -996,33 +1000,36 @@ class LossEvaluator:
                 for ev in done[par]:
                     main.wait_event(ev)
             slots = [self._uslot(par, k, n, P) for k in range(len(idx))]
-            # 1. the sets' per-Gaussian stage (main stream); a view without its depth order sorts it with set 0
-            fresh = [k for k, i in enumerate(idx) if self._orders[i] is None]
-            for k in fresh:
-                i = idx[k]
-                self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
-                check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(gs[0]),
-                                                  slots[k]["geoms"][0].data_ptr(), slots[k]["geoms"][0].numel(), None,
-                                                  self._orders[i].data_ptr(), 1, main_h), "gslm_preprocess_ordered")
+            # 1. each view's depth order (sorted once while xyz is unchanged) and its inverse, the depth positions
+            for k, i in enumerate(idx):
+                if self._orders[i] is None:  # the sort of set 0's geometry (its records are rewritten below)
+                    self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                    check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(gs[0]),
+                                                      slots[k]["geoms"][0].data_ptr(), slots[k]["geoms"][0].numel(),
+                                                      None, self._orders[i].data_ptr(), 1, main_h),
+                          "gslm_preprocess_ordered")
+                    self._pos[i] = None
+                if self._pos[i] is None:
+                    self._pos[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                    check(lib.gslm_depth_positions(self._orders[i].data_ptr(), P, self._pos[i].data_ptr(), main_h),
+                          "gslm_depth_positions")
+            # 2. the sets' render records in depth space: one pass over the Gaussians per set for the batch's views
+            vws = (_lib.GslmView * len(idx))(*[self.views[i] for i in idx])
+            pos = (ctypes.c_void_p * len(idx))(*[self._pos[i].data_ptr() for i in idx])
             for a in range(n):
-                ks = [k for k in range(len(idx)) if not (a == 0 and k in fresh)]
-                if not ks:
-                    continue
-                vws = (_lib.GslmView * len(ks))(*[self.views[idx[k]] for k in ks])
-                ge = (ctypes.c_void_p * len(ks))(*[slots[k]["geoms"][a].data_ptr() for k in ks])
-                check(lib.gslm_preprocess_views(vws, len(ks), ctypes.byref(gs[a]), ge, slots[ks[0]]["geoms"][a].numel(),
-                                                main_h), "gslm_preprocess_views")
-            # 2. union geometries and their pair counts (main stream; the read-back waits for main only)
+                ge = (ctypes.c_void_p * len(idx))(*[sl["geoms"][a].data_ptr() for sl in slots])
+                check(lib.gslm_preprocess_views(vws, len(idx), ctypes.byref(gs[a]), ge, slots[0]["geoms"][a].numel(),
+                                                pos, main_h), "gslm_preprocess_views")
+            # 3. union geometries and their pair counts (main stream; the read-back waits for main only)
             for k, i in enumerate(idx):
                 ge = (ctypes.c_void_p * n)(*[slots[k]["geoms"][a].data_ptr() for a in range(n)])
-                check(lib.gslm_union_geometry(ctypes.byref(self.views[i]), P, ge, n, self._orders[i].data_ptr(),
-                                              slots[k]["ugeom"].data_ptr(), slots[k]["ugeom"].numel(), main_h),
-                      "gslm_union_geometry")
+                check(lib.gslm_union_geometry(ctypes.byref(self.views[i]), P, ge, n, slots[k]["ugeom"].data_ptr(),
+                                              slots[k]["ugeom"].numel(), main_h), "gslm_union_geometry")
             ugeoms = (ctypes.c_void_p * len(idx))(*[sl["ugeom"].data_ptr() for sl in slots])
             Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
             Ns = (ctypes.c_int64 * len(idx))()
             check(lib.gslm_num_rendered_many(ugeoms, Ps, len(idx), Ns, main_h), "gslm_num_rendered_many")
-            # 3. binning + the n blends of each view on its side stream
+            # 4. binning + the n blends of each view on its side stream
             for st in side:
                 st.wait_stream(main)
             for k, (sl, i) in enumerate(zip(slots, idx)):

@@ -121,10 +121,14 @@ int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* g, void
                             int32_t* out_radii, uint32_t* depth_order, int32_t order_mode, void* stream);
 /* The per-Gaussian stage of gslm_preprocess for nviews <= 8 views in one pass over the Gaussians (ABI 8): each view's
  * render records, depth keys, tile counts and rects into geoms[b] (each >= gslm_geom_bytes(P)), bitwise as
- * gslm_preprocess writes them, with no depth sort and no tile-count scan (the line search's parameter sets:
- * gslm_union_geometry consumes only those).  A Gaussian's 236 B of inputs (SH 3) are read once for the views. */
+ * gslm_preprocess writes them, with no depth sort and no tile-count scan.  A Gaussian's 236 B of inputs (SH 3) are
+ * read once for the views.  depth_pos (or NULL): per view the Gaussians' depth positions (gslm_depth_positions of the
+ * view's depth order); then only the render records are written, each at its Gaussian's depth position, the rect
+ * slot zero when culled -- the DEPTH SPACE the line search's union binning reads (below). */
 int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, void* const* geoms,
-                          size_t geom_bytes, void* stream);
+                          size_t geom_bytes, const uint32_t* const* depth_pos, void* stream);
+/* depth_pos[depth_order[s]] = s for s < P (the inverse of a gslm_preprocess_ordered depth order). */
+int gslm_depth_positions(const uint32_t* depth_order, int64_t P, uint32_t* depth_pos, void* stream);
 /* Synchronous read of the number of (tile, Gaussian) pairs produced by gslm_preprocess. */
 int gslm_num_rendered(const void* geom, int64_t P, int64_t* out_num_rendered, void* stream);
 /* The same for n preprocessed geometries (geoms[k] over Ps[k] Gaussians) with ONE stream synchronisation:
@@ -169,19 +173,20 @@ int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* str
  * point, and each point's exact point list is the subsequence of one list binned over the union of the points' rects:
  * the entries whose tile lies in that point's rect, in the same (tile, depth, index) order.  So a view is binned once
  * for the six points instead of once per point (gslm.lm.LossEvaluator.evaluate_points):
- *   1. each point's per-Gaussian stage into its own geometry workspace (geoms[a]: gslm_preprocess_views, or
- *      gslm_preprocess_ordered, which also writes the view's depth order);
- *   2. gslm_union_geometry: the union of the n <= 8 points' rects per Gaussian into union_geom, its tile counts scanned
- *      in depth order -- gslm_num_rendered(union_geom) is the union list's length N;
+ *   1. each point's render records in depth space, in its own geometry workspace (geoms[a]: gslm_preprocess_views
+ *      with the view's depth positions; the depth order from one gslm_preprocess_ordered, order_mode 1);
+ *   2. gslm_union_geometry: the union of the n <= 8 points' rects per depth position into union_geom, the tile counts
+ *      scanned -- gslm_num_rendered(union_geom) is the union list's length N;
  *   3. gslm_union_binning (workspace >= gslm_union_binning_bytes(N, H, W)): duplicate + tile sort + ranges of the union
  *      list, each entry carrying 4 bits per point through the sort (slot a: the point's quadrant mask of the entry --
  *      the bits its own binning would give it -- and 0 when its tile is outside the point's rect or the Gaussian is
  *      culled there);
  *   4. gslm_rasterize_loss_slot(geom = geoms[a], slot = a): gslm_rasterize_loss's blend + loss over the entries of
- *      slot a -- the same visits in the same order with the same records as the exact render: the same loss, bitwise. */
+ *      slot a -- the same visits in the same order with the same records as the exact render: the same loss, bitwise.
+ * The union list's values are depth positions (every pass reads the points' records coalesced in depth order). */
 size_t gslm_union_binning_bytes(int64_t num_rendered, int32_t H, int32_t W);
-int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n,
-                        const uint32_t* depth_order, void* union_geom, size_t union_geom_bytes, void* stream);
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, void* union_geom,
+                        size_t union_geom_bytes, void* stream);
 int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,
                        int64_t num_rendered, const void* const* geoms, int32_t n, void* stream);
 int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, const void* binning,

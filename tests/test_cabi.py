@@ -101,13 +101,16 @@ def test_union_binning_argument_checks():
     geoms = (ctypes.c_void_p * 9)(*([None] * 9))
     gb = lib.gslm_geom_bytes(10)
     for n in (0, 9):
-        assert lib.gslm_union_geometry(vp, 10, geoms, n, 16, 16, gb, None) == _lib.GSLM_ERR_INVALID
+        assert lib.gslm_union_geometry(vp, 10, geoms, n, 16, gb, None) == _lib.GSLM_ERR_INVALID
         assert b"parameter sets" in lib.gslm_last_error()
-    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, 16, gb - 1, None) == _lib.GSLM_ERR_CAPACITY
-    assert lib.gslm_union_geometry(vp, 10, geoms, 2, None, 16, gb, None) == _lib.GSLM_ERR_INVALID
-    assert b"depth_order" in lib.gslm_last_error()
-    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, 16, gb, None) == _lib.GSLM_ERR_INVALID
+    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, gb - 1, None) == _lib.GSLM_ERR_CAPACITY
+    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, gb, None) == _lib.GSLM_ERR_INVALID
     assert b"NULL geometry" in lib.gslm_last_error()
+    assert lib.gslm_depth_positions(None, 10, None, None) == _lib.GSLM_ERR_INVALID
+    views = (_lib.GslmView * 9)(*([view] * 9))
+    g = _lib.make_gaussians(0)
+    for n in (0, 9):
+        assert lib.gslm_preprocess_views(views, n, ctypes.byref(g), geoms, gb, None, None) == _lib.GSLM_ERR_INVALID
     # the union list carries two more words per entry than a binning (the per-set masks' sort ping-pong)
     nb = lib.gslm_union_binning_bytes(100, 64, 64)
     assert nb >= lib.gslm_binning_bytes(100, 64, 64) + 2 * 100 * 4

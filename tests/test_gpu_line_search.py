@@ -157,7 +157,8 @@ def test_union_lm_step_matches_reference_golden():
 @pytest.mark.parametrize("nviews", [1, 3, 8])
 def test_preprocess_views_equals_per_view_preprocess(nviews):
     """gslm_preprocess_views (one pass over the Gaussians for several views) writes each view's records, tile counts
-    and rects bitwise as gslm_preprocess does (ragged P, mixed image sizes)."""
+    and rects bitwise as gslm_preprocess does (ragged P, mixed image sizes); with depth positions, the same records at
+    each Gaussian's depth position (the rect slot zero when culled)."""
     import ctypes
     from gslm import _lib
     from gslm.cameras import orbit_cameras
@@ -176,7 +177,7 @@ def test_preprocess_views_equals_per_view_preprocess(nviews):
     for k in range(nviews):
         assert lib.gslm_preprocess(ctypes.byref(views[k]), ctypes.byref(g), a[k].data_ptr(), nb, None, None) == 0
     ge = (ctypes.c_void_p * nviews)(*[t.data_ptr() for t in b])
-    assert lib.gslm_preprocess_views(views, nviews, ctypes.byref(g), ge, nb, None) == 0, lib.gslm_last_error()
+    assert lib.gslm_preprocess_views(views, nviews, ctypes.byref(g), ge, nb, None, None) == 0, lib.gslm_last_error()
     torch.cuda.synchronize()
     P = g.P
     rec = 64 * P  # render records [P][4] float4
@@ -194,6 +195,32 @@ def test_preprocess_views_equals_per_view_preprocess(nviews):
         rect_a = a[k][r0:r0 + 8 * P].view(torch.int64)
         rect_b = b[k][r0:r0 + 8 * P].view(torch.int64)
         assert torch.equal(rect_a[vis], rect_b[vis])
+    # depth space: each view's records at its Gaussians' depth positions, the rect slot zero when culled
+    orders, poss, c = [], [], [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(nviews)]
+    for k in range(nviews):
+        o = torch.empty(P, dtype=torch.int32, device="cuda")
+        assert lib.gslm_preprocess_ordered(ctypes.byref(views[k]), ctypes.byref(g), a[k].data_ptr(), nb, None,
+                                           o.data_ptr(), 1, None) == 0
+        pos = torch.empty(P, dtype=torch.int32, device="cuda")
+        assert lib.gslm_depth_positions(o.data_ptr(), P, pos.data_ptr(), None) == 0
+        orders.append(o)
+        poss.append(pos)
+    pp = (ctypes.c_void_p * nviews)(*[t.data_ptr() for t in poss])
+    gc = (ctypes.c_void_p * nviews)(*[t.data_ptr() for t in c])
+    assert lib.gslm_preprocess_views(views, nviews, ctypes.byref(g), gc, nb, pp, None) == 0, lib.gslm_last_error()
+    torch.cuda.synchronize()
+    for k in range(nviews):
+        o = orders[k].long()
+        assert torch.equal(poss[k].long()[o], torch.arange(P, device="cuda"))  # pos is the order's inverse
+        ra = b[k][:rec].view(torch.float32).view(P, 16)
+        rc = c[k][:rec].view(torch.float32).view(P, 16)[poss[k].long()]  # back in index order
+        tiles = b[k][_off(rec, keys):_off(rec, keys) + keys].view(torch.int32)
+        vis = tiles > 0
+        assert torch.equal(rc[vis][:, :12].view(torch.int32), ra[vis][:, :12].view(torch.int32))
+        r0 = _off(rec, keys) + _al(keys)
+        rect = b[k][r0:r0 + 8 * P].view(torch.int64)
+        assert torch.equal(rc[vis][:, 12:14].contiguous().view(torch.int64).reshape(-1), rect[vis])
+        assert bool((rc[~vis][:, 12:14] == 0).all())
 
 
 def _al(x):

@@ -13,3 +13,7 @@ find $GRAFT_REPO_ROOT/$O/prof -name "*stats*"
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u tools/exp/dropin_breakdown.py > $O/dropin.json 2> $O/dropin.err || { echo "dropin failed"; tail -20 $O/dropin.err; exit 1; }
 cat $O/dropin.json
+if [ "${BENCH:-0}" = "1" ]; then
+  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+  cat $O/bench.json
+fi
