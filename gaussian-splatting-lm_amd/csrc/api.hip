@@ -474,6 +474,38 @@ int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom,
                             (hipStream_t)stream, N > 0 ? um.sorted : nullptr, 4 * slot);
 }
 
+size_t gslm_loss_sets_scratch_bytes(int32_t n, int32_t H, int32_t W) {
+  return (size_t)(n > 0 ? n : 1) * gslm_loss_scratch_bytes(H, W);
+}
+
+int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, const void* binning,
+                             size_t binning_bytes, int64_t N, const float* gt, const float* alpha_mask, void* scratch,
+                             size_t scratch_bytes, double* const* loss_dev, int32_t accumulate, void* stream) {
+  ViewK v;
+  int st = make_view(view, 1, &v);
+  if (st) return st;
+  if (n < 1 || n > MAX_UNION_SETS) { set_error("rasterize_loss_sets: 1 <= n <= 8 parameter sets"); return GSLM_ERR_INVALID; }
+  if (N < 0 || N > 0xFFFFFFFFll) { set_error("rasterize_loss_sets: N out of range"); return GSLM_ERR_INVALID; }
+  if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
+  if (scratch_bytes < gslm_loss_sets_scratch_bytes(n, v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
+  if (!gt || !loss_dev || !scratch || !geoms) { set_error("rasterize_loss_sets: NULL gt / loss / scratch / geoms"); return GSLM_ERR_INVALID; }
+  SetRecsK sr{};
+  LossPtrsK lp{};
+  for (int a = 0; a < n; ++a) {
+    if ((P && !geoms[a]) || !loss_dev[a]) { set_error("rasterize_loss_sets: NULL geometry / loss"); return GSLM_ERR_INVALID; }
+    GeomBufs gb;
+    geom_layout(P, const_cast<void*>(geoms[a]), &gb);
+    sr.rec[a] = gb.rec;
+    lp.loss[a] = loss_dev[a];
+  }
+  BinBufs bb;
+  UnionMasks um;
+  bin_layout(N, v.gx * v.gy, const_cast<void*>(binning), &bb);
+  union_masks_layout(N, v.gx * v.gy, const_cast<void*>(binning), &um);
+  return launch_render_loss_sets(v, sr, n, bb, um.sorted, gt, alpha_mask, (double*)scratch, lp, accumulate ? 1 : 0,
+                                 (hipStream_t)stream);
+}
+
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream) {
   if (!dst || (P > 0 && !geom)) { set_error("num_rendered_copy: NULL geom / dst"); return GSLM_ERR_INVALID; }
   if (P == 0) {

@@ -482,6 +482,16 @@ struct UnionMasks {
   uint32_t* sorted;
 };
 size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* out);
+// all sets' blends + losses over a union list in one pass (render_fwd.hip, gslm_rasterize_loss_sets)
+struct SetRecsK {
+  const float4* rec[MAX_UNION_SETS];
+};
+struct LossPtrsK {
+  double* loss[MAX_UNION_SETS];
+};
+int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const BinBufs& bb, const uint32_t* amask,
+                            const float* gt, const float* mask, double* part, const LossPtrsK& lp, int accumulate,
+                            hipStream_t s);
 int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s);
 int launch_depth_positions(int64_t P, const uint32_t* order, uint32_t* pos, hipStream_t s);
 int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,

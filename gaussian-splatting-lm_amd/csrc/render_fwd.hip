@@ -126,6 +126,188 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
   }
 }
 
+// The line search's union list blended for all NS parameter sets in ONE pass (gslm_rasterize_loss_sets): per wave the
+// list is walked once -- each round's 64 entries and their mask words loaded once -- and set a's round is
+// k_render_fwd_wave<FWD_LOSS, true>'s round for slot a: its hits (bit 4a + q) staged from set a's records, the same
+// visit arithmetic on set a's own pixel state, the same per-set stop.  Set a + 1's records are loaded while set a's
+// hits are visited, so a round waits on two dependent loads (entries, set 0's records) instead of two per set.
+// Every set's visits and their order are the single-set kernel's: the same losses, bitwise.
+template <int NS>
+__global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* __restrict__ ranges,
+                                                           const uint32_t* __restrict__ tile_order,
+                                                           const uint32_t* __restrict__ point_list,
+                                                           const uint32_t* __restrict__ amask, SetRecsK sr,
+                                                           const float* __restrict__ gt, const float* __restrict__ mask,
+                                                           double* __restrict__ part) {
+  __shared__ float4 s_rec[4][3 * 64];
+  const int tile = (int)tile_order[blockIdx.x];
+  const int tile_x = tile % v.gx, tile_y = tile / v.gx;
+  const int tid = threadIdx.x, q = tid >> 6, lane = tid & 63;
+  int px, py;
+  tile_pixel(tile_x, tile_y, tid, px, py);
+  const bool inside = px < v.W && py < v.H;
+  const float pxf = (float)px, pyf = (float)py;
+  const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
+  const uint32_t* pl = point_list + range.x;
+  const uint32_t* am = amask + range.x;
+  float4* s = s_rec[q];
+  float T[NS], Tstop[NS], C0[NS], C1[NS], C2[NS];
+  uint64_t dmask[NS];
+  const uint64_t out0 = __builtin_amdgcn_ballot_w64(!inside);
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    T[a] = inside ? 1.0f : 0.0f;
+    Tstop[a] = 0.0f;
+    C0[a] = C1[a] = C2[a] = 0.f;
+    dmask[a] = out0;
+  }
+  for (int base = 0; base < n; base += 64) {
+    bool all = true;
+#pragma unroll
+    for (int a = 0; a < NS; ++a) all = all && dmask[a] == ~0ull;
+    if (all) break;  // every pixel of this quadrant has stopped in every set
+    const int k = base + lane;
+    uint32_t g = 0u, m = 0u;
+    if (k < n) {
+      g = pl_id(pl[k]);
+      m = am[k];
+    }
+    // set 0's records of this lane's entry (if it is a hit of a set still blending)
+    bool hit = dmask[0] != ~0ull && ((m >> q) & 1u);
+    float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
+    if (hit) {
+      const float4* r = sr.rec[0] + RECS * (size_t)g;
+      ra = r[0];
+      rb = r[1];
+      rc = r[2];
+    }
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
+      if (hit) {
+        s[lane] = ra;
+        s[64 + lane] = rb;
+        s[128 + lane] = rc;
+      }
+      uint64_t hb = __ballot(hit);
+      wave_lds_sync();
+      if (a + 1 < NS) {  // the next set's records while this set's hits are visited
+        hit = dmask[a + 1] != ~0ull && ((m >> (4 * (a + 1) + q)) & 1u);
+        if (hit) {
+          const float4* r = sr.rec[a + 1] + RECS * (size_t)g;
+          ra = r[0];
+          rb = r[1];
+          rc = r[2];
+        }
+      }
+      float Ta = T[a], Tsa = Tstop[a], c0 = C0[a], c1 = C1[a], c2 = C2[a];
+      uint64_t dm = dmask[a];
+      while (hb) {
+        const int j = (int)__builtin_ctzll(hb);
+        hb &= hb - 1ull;
+        const float4 x = s[j], y = s[64 + j], z = s[128 + j];
+        asm volatile("" : : "v"(y.z), "v"(y.w), "v"(z.x));
+        const float dx = x.x - pxf, dy = x.y - pyf;
+        const float power = gpower(x.z, x.w, y.x, dx, dy);
+        const float alpha = fminf(0.99f, y.y * gexp(power));
+        float u = alpha >= 1.0f / 255.0f ? alpha : 0.0f;
+        u = power > 0.0f ? 0.0f : u;
+        const float test_T = Ta * (1.0f - u);
+        const bool stop = test_T < 0.0001f;
+        const float wt = stop ? 0.0f : u * Ta;
+        c0 += y.z * wt;
+        c1 += y.w * wt;
+        c2 += z.x * wt;
+        Tsa = stop ? Tsa + Ta : Tsa;
+        Ta = stop ? 0.0f : test_T;
+        dm |= __builtin_amdgcn_ballot_w64(stop);
+        if (dm == ~0ull) break;
+      }
+      T[a] = Ta;
+      Tstop[a] = Tsa;
+      C0[a] = c0;
+      C1[a] = c1;
+      C2[a] = c2;
+      dmask[a] = dm;
+      wave_lds_sync();  // this set's hits read before the next set's are staged
+    }
+  }
+  const int64_t pid = (int64_t)py * v.W + px;
+  const int64_t HW = (int64_t)v.H * v.W;
+  __shared__ double s_sum[NS][4];
+  float gtc[3] = {0.f, 0.f, 0.f};
+  float mv = 1.0f;
+  if (inside) {
+    mv = mask ? mask[pid] : 1.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gtc[c] = gt[c * HW + pid];
+  }
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double acc = 0.0;
+    if (inside) {
+      const float Tf = T[a] > 0.0f ? T[a] : Tstop[a];
+      const float R[3] = {C0[a] + Tf * v.bg[0], C1[a] + Tf * v.bg[1], C2[a] + Tf * v.bg[2]};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float r = mv * fminf(fmaxf(R[c], 0.0f), 1.0f) - gtc[c];
+        acc += (double)r * (double)r;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0) s_sum[a][q] = acc;
+  }
+  __syncthreads();
+  if (tid < NS) part[(int64_t)tid * (v.gx * v.gy) + tile] = ((s_sum[tid][0] + s_sum[tid][1]) + s_sum[tid][2]) + s_sum[tid][3];
+}
+
+// per set a (block a): the sum of its per-tile partials in tile order, times 2, into *loss[a] (k_tile_loss_final)
+__global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __restrict__ part, int np, int accumulate,
+                                                               LossPtrsK lp) {
+  __shared__ double s[4];
+  const int a = blockIdx.x;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[(int64_t)a * np + i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    double* out = lp.loss[a];
+    *out = accumulate ? *out + l : l;
+  }
+}
+
+int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const BinBufs& bb, const uint32_t* amask,
+                            const float* gt, const float* mask, double* part, const LossPtrsK& lp, int accumulate,
+                            hipStream_t s) {
+  const int ntiles = v.gx * v.gy;
+  if (ntiles == 0) {
+    if (!accumulate)
+      for (int a = 0; a < nsets; ++a) GSLM_HIP_CHECK(hipMemsetAsync(lp.loss[a], 0, sizeof(double), s));
+    return GSLM_OK;
+  }
+  const dim3 grid(ntiles), block(TILE_PIX);
+  switch (nsets) {
+#define GSLM_LOSS_SETS(NS)                                                                                           \
+  case NS:                                                                                                           \
+    hipLaunchKernelGGL(k_render_loss_sets<NS>, grid, block, 0, s, v, bb.ranges, bb.tile_order, bb.point_list, amask, \
+                       sr, gt, mask, part);                                                                          \
+    break;
+    GSLM_LOSS_SETS(1) GSLM_LOSS_SETS(2) GSLM_LOSS_SETS(3) GSLM_LOSS_SETS(4)
+    GSLM_LOSS_SETS(5) GSLM_LOSS_SETS(6) GSLM_LOSS_SETS(7) GSLM_LOSS_SETS(8)
+#undef GSLM_LOSS_SETS
+    default:
+      set_error("rasterize_loss_sets: 1..8 parameter sets");
+      return GSLM_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(k_tile_loss_final_sets, dim3(nsets), dim3(256), 0, s, (const double*)part, ntiles, accumulate, lp);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 // sum of the per-tile loss partials in tile order (deterministic), times 2 (the [r; r] aliasing)
 __global__ __launch_bounds__(256) void k_tile_loss_final(const double* __restrict__ part, int np, int accumulate,
                                                           double* __restrict__ loss) {

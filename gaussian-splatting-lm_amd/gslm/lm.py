@@ -17,6 +17,7 @@ the same iterates in exact arithmetic; the reference's restart schedule and stop
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -819,6 +820,10 @@ class LossEvaluator:
         # geometry and the union list
         self.uslots = [[dict(geoms=[], ugeom=None) for _ in range(self.batch)] for _ in range(2)]
         self.ubins = [None] * self.batch
+        self.sets_scratch = [None] * self.batch
+        # the six points' blends: one pass over each union list for all sets (gslm_rasterize_loss_sets), or one pass per
+        # set (gslm_rasterize_loss_slot; GSLM_LOSS_SETS=0) -- the same losses bitwise
+        self.loss_sets = os.environ.get("GSLM_LOSS_SETS", "1") != "0"
         self.union_counts = []
 
     def _slot(self, k, P):
@@ -949,6 +954,14 @@ class LossEvaluator:
         return loss
 
     # ---- the line search's six points with one binning per view (include/gslm.h "shared binning", ABI 8) ----
+    def _sets_scratch(self, k, n, H, W):
+        """Batch position k's per-tile partials of the all-sets blend (its stream's own buffer)."""
+        nb = lib.gslm_loss_sets_scratch_bytes(n, H, W)
+        t = self.sets_scratch[k]
+        if t is None or t.numel() * 8 < nb:
+            t = self.sets_scratch[k] = torch.empty(nb // 8 + 1, dtype=torch.float64, device=self.device)
+        return t
+
     def _uslot(self, par, k, n, P):
         """Batch position k's geometries (n sets) and union geometry, of slot set `par` (two sets alternate over the
         batches: a batch's preprocesses overwrite the slots of the batch before the previous one)."""
@@ -1048,6 +1061,14 @@ class LossEvaluator:
                 check(lib.gslm_union_binning(ctypes.byref(vw), P, sl["ugeom"].data_ptr(), binning.data_ptr(),
                                              binning.numel(), N, ge, n, sh), "gslm_union_binning")
                 m = self.masks[i]
+                if self.loss_sets:  # all sets in one pass over the union list
+                    scr = self._sets_scratch(k, n, H, W)
+                    lp = (ctypes.c_void_p * n)(*[losses[a].data_ptr() + 8 * i for a in range(n)])
+                    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, binning.data_ptr(), binning.numel(), N,
+                                                       self.gts[i].data_ptr(), None if m is None else m.data_ptr(),
+                                                       scr.data_ptr(), scr.numel() * 8, lp, 0, sh),
+                          "gslm_rasterize_loss_sets")
+                    continue
                 scr = self.loss_scratch[k % len(self.streams)]
                 for a in range(n):
                     check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][a].data_ptr(), binning.data_ptr(),

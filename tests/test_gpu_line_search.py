@@ -76,6 +76,10 @@ def test_evaluate_points_equal_exact_renders(batch, streams):
     for i, N in enumerate(ev_u.union_counts):
         assert N >= max(c[i] for c in counts)
     assert any(N > min(c[i] for c in counts) for i, N in enumerate(ev_u.union_counts))
+    # the per-set blends (one pass per set) give the same losses as the all-sets pass
+    ev_u.loss_sets = False
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+    ev_u.loss_sets = True
     # fewer points, and a second LM step on the same evaluator (buffers reused, depth orders cached)
     assert [float(x) for x in ev_u.evaluate_points(sets[2:5])] == exact[2:5]
     sets2, exact2, _, _ = _points(m, lay, s, ev_x)
