@@ -39,6 +39,15 @@ def main():
             "y_max": float((got["y"] - ref["y"]).abs().max() / ref["y"].abs().max()),
             "x_rel": float((got["x"] - ref["x"]).norm() / ref["x"].norm()),
         }
+        if mode == "gaussian":
+            # two views per rank: the product ran pipelined (async all-to-alls per view group); the unpipelined
+            # schedule must give the same product and iterates, bitwise
+            out["exchanges"][mode]["pipelined"] = bool(op._overlap() and op.per > 1)
+            os.environ["GSLM_OVERLAP"] = "0"
+            sync = _run(op, op.layout, v=got.get("v"))
+            del os.environ["GSLM_OVERLAP"]
+            out["exchanges"][mode]["pipelined_bitwise"] = bool(torch.equal(sync["y"], got["y"]) and
+                                                               torch.equal(sync["x"], got["x"]))
     # the whole LM step (train_jvp.py:237-279) on the sharded path: Gaussian-sharded CG + all-reduced line search
     import numpy as np
     from gslm.lm import lm_step

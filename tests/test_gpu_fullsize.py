@@ -210,3 +210,51 @@ def test_fullsize_lm_matvec(name):
         err = _rel_err(got, ref)
         assert err < 1e-4, f"group {gname}: rel err {err:.3e}"
     assert y[o["xyz"][0]:o["xyz"][1]].abs().max() == 0
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_fullsize_forward_whole_frame(name):
+    """The blend over EVERY tile of the 1080p frame (not a sample): n_contrib bit-exact at every pixel, colour and
+    inverse depth within 1e-4, final_T within 1e-5 (the oracle's dense blend, ~3 s at 100k, ~30 s at 1M on 16 host
+    threads)."""
+    from test_gpu_raster import _gpu_forward_internals
+    model, cam = _scene(CONFIGS[name])
+    a = activated(model)
+    st = oracle_settings(cam, 3)
+    with torch.no_grad():
+        pre = tr.preprocess(a["means3D"], torch.zeros_like(a["means3D"]), a["opacities"], a["shs"], None,
+                            a["scales"], a["rotations"], None, st)
+        pl, _, ranges = tr.binning(pre)
+        color, invd, fT, nc = tr.blend(pre, pl, ranges, H, W, st.bg)
+    G = _gpu_forward_internals(model, cam, 3)
+    assert torch.equal(G["n_contrib"].long(), nc.long()), "n_contrib must match exactly at every pixel"
+    assert (G["final_T"] - fT).abs().max() <= 1e-5
+    assert (G["color"] - color).abs().max() <= 1e-4
+    assert (G["invdepth"] - invd).abs().max() <= 1e-4
+
+
+def test_fullsize_backward_whole_frame_100k():
+    """configs[1]'s backward with dL/dcolor ~ N(0, 1) over the WHOLE frame against the oracle's autograd through every
+    tile (every Gaussian's gradient, 1e-4 of each tensor's max)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    model, cam = _scene(CONFIGS["cfg1_100k_sh3_1080p"])
+    a0 = activated(model)
+    st = oracle_settings(cam, 3)
+    dcol = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4))
+    a = {k: v.clone().requires_grad_(True) for k, v in a0.items()}
+    m2 = torch.zeros_like(a0["means3D"], requires_grad=True)
+    pre = tr.preprocess(a["means3D"], m2, a["opacities"], a["shs"], None, a["scales"], a["rotations"], None, st)
+    pl, _, ranges = tr.binning(pre)
+    color, _, _, _ = tr.blend(pre, pl, ranges, H, W, st.bg)
+    (color * dcol).sum().backward()
+    ref = {k: v.grad for k, v in a.items()} | {"means2D": m2.grad}
+    ag = {k: v.to(DEV).requires_grad_(True) for k, v in a0.items()}
+    m2g = torch.zeros_like(ag["means3D"], requires_grad=True)
+    c, _, _ = GaussianRasterizer(gpu_settings(cam, 3))(means3D=ag["means3D"], means2D=m2g, shs=ag["shs"],
+                                                       opacities=ag["opacities"], scales=ag["scales"],
+                                                       rotations=ag["rotations"])
+    c.backward(dcol.to(DEV))
+    got = {k: v.grad.cpu() for k, v in ag.items()} | {"means2D": m2g.grad.cpu()}
+    for k in ref:
+        err = _rel_err(got[k], ref[k])
+        assert err < 1e-4, f"grad {k}: rel err {err:.3e}"

@@ -30,6 +30,9 @@ def test_exchanges_through_rccl_one_rank():
         assert e["g_max"] <= 1e-5, (mode, e)
         assert e["y_max"] <= 1e-5, (mode, e)
         assert e["x_rel"] <= 1e-4, (mode, e)
+    # two views per rank: the product ran pipelined (async all-to-alls per view group), bitwise the synchronous one
+    assert res["exchanges"]["gaussian"]["pipelined"], res["exchanges"]["gaussian"]
+    assert res["exchanges"]["gaussian"]["pipelined_bitwise"], res["exchanges"]["gaussian"]
     lm = res["lm_step"]  # the sharded LM step through RCCL against the reference's (lm_step_golden.npz)
     assert lm["ranks"] == 1 and lm["best_alpha"] == lm["best_alpha_ref"], lm
     assert lm["step_rel"] <= 1e-4 and lm["final_rel"] <= 1e-4, lm

@@ -57,6 +57,10 @@ local = LMProblem(model, mine, torch.zeros(3), device=dev, sh_projection=False)
 local.evaluate()
 op = GaussianShardedOperator(local, all_cams=cams, emulate=(r, n))
 op._exchange_flags()
+# visible fraction of the shard's Gaussians per view (the flags' top bit): what compressing the exchange to visible
+# Gaussians (batch_render.py:124 viewcount > 0) could save
+fl = op._buffers()["flags"]
+out["visible_frac"] = [round(float(((fl[k] >> 31) != 0).float().mean()), 4) for k in range(fl.shape[0])]
 gs = op.rhs(op.zeros())
 t_warm = time.perf_counter()
 while time.perf_counter() - t_warm < 1.0:  # clocks: ~1 s of CG load first
