@@ -42,12 +42,20 @@ def main():
         if mode == "gaussian":
             # two views per rank: the product ran pipelined (async all-to-alls per view group); the unpipelined
             # schedule must give the same product and iterates, bitwise
+            from gslm.lm import cgls_fused
             out["exchanges"][mode]["pipelined"] = bool(op._overlap() and op.per > 1)
-            os.environ["GSLM_OVERLAP"] = "0"
-            sync = _run(op, op.layout, v=got.get("v"))
+            vs = op.shard(got["v"].cuda())
+            g = op.rhs(op.zeros())
+            res = []
+            for flag in ("1", "0"):
+                os.environ["GSLM_OVERLAP"] = flag
+                y = op.matvec(vs, op.zeros())
+                x, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=False)
+                torch.cuda.synchronize()
+                res.append((y.clone(), x.clone()))
             del os.environ["GSLM_OVERLAP"]
-            out["exchanges"][mode]["pipelined_bitwise"] = bool(torch.equal(sync["y"], got["y"]) and
-                                                               torch.equal(sync["x"], got["x"]))
+            out["exchanges"][mode]["pipelined_bitwise"] = bool(torch.equal(res[0][0], res[1][0]) and
+                                                               torch.equal(res[0][1], res[1][1]))
     # the whole LM step (train_jvp.py:237-279) on the sharded path: Gaussian-sharded CG + all-reduced line search
     import numpy as np
     from gslm.lm import lm_step

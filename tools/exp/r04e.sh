@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r04e}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -k "${KEXPR:-line_search or lm_step}" > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -rP -k "${KEXPR:-line_search or lm_step}" > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
 tail -3 $O/gpu_tests.log
 timeout -k 10 300 python -u tools/exp/ls_union.py --reps 3 > $O/ls.json 2> $O/ls.err || { echo "ls failed"; tail -20 $O/ls.err; exit 1; }
 cat $O/ls.json
