@@ -195,6 +195,7 @@ size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* o) {
   UnionMasks m;
   m.m0 = c.take<uint32_t>(N);
   m.m1 = c.take<uint32_t>(N);
+  m.hist = c.take<uint32_t>(sort_hist_bytes(N, true) / 4);
   m.sorted = (bb.passes & 1) ? m.m1 : m.m0;
   if (o) *o = m;
   return c.off;

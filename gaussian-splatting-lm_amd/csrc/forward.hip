@@ -464,72 +464,96 @@ __global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint
   urect[i] = any ? make_uint2(x0 | (y0 << 16), x1 | (y1 << 16)) : make_uint2(0u, 0u);
 }
 
-// k_duplicate over the union rects in depth space (the same emission as k_duplicate: one block per 256 depth
+// k_duplicate over the union rects in depth space (the same emission as k_duplicate: one block per DUPU_G depth
 // positions, elements in order, a Gaussian's rect row-major), the value the depth position with quadrant bits 0xF,
-// and amask[e] = bits 4a..4a+3 the quadrant mask of set a.  Each set's record of the block's Gaussians (coalesced in
-// depth space) is staged in LDS once ([x y a b], [c tq rect]: 32 B) and the masks are evaluated per element.
-// Dynamic LDS: NS * 256 * 32 B.
+// and amask[e] = bits 4a..4a+3 the quadrant mask of set a.  Each (Gaussian, set) quadrant test is prepared once
+// (quad_cull_prep on the set's record, read coalesced in depth space) into LDS -- [ia b det ta] [ydom yr sqm mode]
+// and the set's rect -- and every element evaluates quad_mask on it: the bits k_duplicate writes for that set's own
+// list.  (Preparing per element was 6 square roots and 4 divisions per set and entry: 252 us per 1080p view at 1M,
+// 5x the plain k_duplicate.)  The centre is the same in every set that keeps the Gaussian (the points share xyz and
+// the view), so its copy in s_gxy is written by each such set with the same bits.  Half-size blocks keep the
+// staging at NS * 5 KB of LDS (dynamic: NS * 2 * DUPU_G float4).
+constexpr int DUPU_G = 128;
 template <int NS>
 __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ offsets,
                                                           uint32_t N, const uint2* __restrict__ urect, UnionSets u,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                           uint32_t* __restrict__ amask) {
-  extern __shared__ float4 s_set[];  // [NS][2][256]
-  __shared__ uint32_t s_off[257];
-  __shared__ uint32_t s_rc[256][3];  // x0, y0, width of the union rect
-  const int tid = threadIdx.x;
-  const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
-  const int64_t slast = min(s0 + 255, P - 1);
+  extern __shared__ float4 s_set[];  // [NS][2][DUPU_G]
+  __shared__ uint2 s_srect[NS][DUPU_G];
+  __shared__ float2 s_gxy[DUPU_G];
+  __shared__ uint32_t s_off[DUPU_G + 1];
+  __shared__ uint32_t s_rc[DUPU_G][3];  // x0, y0, width of the union rect
+  const int tid = threadIdx.x, gi = tid & (DUPU_G - 1), half = tid >> 7;
+  const int64_t s0 = (int64_t)blockIdx.x * DUPU_G, s = s0 + gi;
+  const int64_t slast = min(s0 + DUPU_G - 1, P - 1);
   const uint32_t base = offsets[s0];
   uint32_t n = 0;
   if (s < P) {
     const uint32_t o = offsets[s];
     n = (s + 1 < P ? offsets[s + 1] : N) - o;
-    s_off[tid] = o - base;
-    if (n) {
-      const uint2 rc = urect[s];
-      const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
-      s_rc[tid][0] = (uint32_t)x0;
-      s_rc[tid][1] = (uint32_t)y0;
-      s_rc[tid][2] = (uint32_t)(x1 - x0);
-      float4 r0[NS], r3[NS];
-      float r1x[NS], r2w[NS];
-#pragma unroll
-      for (int a = 0; a < NS; ++a) {  // every set's loads in flight together
-        const float4* r = u.rec[a] + RECS * (size_t)s;
-        r0[a] = r[0];
-        r1x[a] = r[1].x;
-        r2w[a] = r[2].w;
-        r3[a] = r[3];
-      }
-#pragma unroll
-      for (int a = 0; a < NS; ++a) {  // a culled set's record holds a zero rect (and stale values: no tile passes)
-        s_set[(2 * a) * 256 + tid] = r0[a];
-        s_set[(2 * a + 1) * 256 + tid] = make_float4(r1x[a], r2w[a], r3[a].x, r3[a].y);
+    if (half == 0) {
+      s_off[gi] = o - base;
+      if (n) {
+        const uint2 rc = urect[s];
+        const int x0 = rc.x & 0xFFFF, y0 = rc.x >> 16, x1 = rc.y & 0xFFFF;
+        s_rc[gi][0] = (uint32_t)x0;
+        s_rc[gi][1] = (uint32_t)y0;
+        s_rc[gi][2] = (uint32_t)(x1 - x0);
       }
     }
-  } else {
-    s_off[tid] = 0xFFFFFFFFu;  // past the block's last Gaussian: never an owner
+    if (n) {
+#pragma unroll
+      for (int k = 0; k < (NS + 1) / 2; ++k) {
+        const int a = 2 * k + half;
+        if (a >= NS) break;
+        const float4* r = u.rec[a] + RECS * (size_t)s;
+        const float4 r0 = r[0], r3 = r[3];
+        const float r1x = r[1].x, r2w = r[2].w;
+        const uint2 rc = make_uint2(__float_as_uint(r3.x), __float_as_uint(r3.y));
+        s_srect[a][gi] = rc;  // zero when set a culls the Gaussian (its other record fields are stale: unused)
+        if (rc.y != 0u) {
+          const QuadCull q = quad_cull_prep(r0.x, r0.y, r0.z, r0.w, r1x, r2w);
+          s_set[(2 * a) * DUPU_G + gi] = make_float4(q.ia, q.b, q.det, q.ta);
+          s_set[(2 * a + 1) * DUPU_G + gi] = make_float4(q.ydom, q.yr, q.sqm, __int_as_float(q.mode));
+          s_gxy[gi] = make_float2(r0.x, r0.y);
+        }
+      }
+    }
+  } else if (half == 0) {
+    s_off[gi] = 0xFFFFFFFFu;  // past the block's last Gaussian: never an owner
   }
-  if (s == slast) s_off[256] = offsets[s] - base + n;
+  if (s == slast && half == 0) s_off[DUPU_G] = offsets[s] - base + n;
   __syncthreads();
-  const uint32_t total = base < N ? min(s_off[256], N - base) : 0u;
+  const uint32_t total = base < N ? min(s_off[DUPU_G], N - base) : 0u;
   for (uint32_t e = tid; e < total; e += 256) {
     int lo = 0;
 #pragma unroll
-    for (int step = 128; step > 0; step >>= 1) lo = s_off[lo + step] <= e ? lo + step : lo;
+    for (int step = DUPU_G / 2; step > 0; step >>= 1) lo = s_off[lo + step] <= e ? lo + step : lo;
     const uint32_t li = e - s_off[lo];
     const uint32_t w = s_rc[lo][2];
     const uint32_t dy = li / w;
     const int tx = (int)(s_rc[lo][0] + (li - dy * w)), ty = (int)(s_rc[lo][1] + dy);
+    const float2 gxy = s_gxy[lo];
     uint32_t m = 0u;
 #pragma unroll
     for (int a = 0; a < NS; ++a) {
-      const float4 r0 = s_set[(2 * a) * 256 + lo], r1 = s_set[(2 * a + 1) * 256 + lo];
-      const uint32_t rlo = __float_as_uint(r1.z), rhi = __float_as_uint(r1.w);
-      if (tx < (int)(rlo & 0xFFFFu) || ty < (int)(rlo >> 16) || tx >= (int)(rhi & 0xFFFFu) || ty >= (int)(rhi >> 16))
+      const uint2 rc = s_srect[a][lo];
+      if (tx < (int)(rc.x & 0xFFFFu) || ty < (int)(rc.x >> 16) || tx >= (int)(rc.y & 0xFFFFu) || ty >= (int)(rc.y >> 16))
         continue;  // outside set a's rect (an empty rect when set a culls the Gaussian)
-      m |= quad_mask(quad_cull_prep(r0.x, r0.y, r0.z, r0.w, r1.x, r1.y), tx, ty) << (4 * a);
+      const float4 qa = s_set[(2 * a) * DUPU_G + lo], qb = s_set[(2 * a + 1) * DUPU_G + lo];
+      QuadCull q;
+      q.gx = gxy.x;
+      q.gy = gxy.y;
+      q.ia = qa.x;
+      q.b = qa.y;
+      q.det = qa.z;
+      q.ta = qa.w;
+      q.ydom = qb.x;
+      q.yr = qb.y;
+      q.sqm = qb.z;
+      q.mode = __float_as_int(qb.w);
+      m |= quad_mask(q, tx, ty) << (4 * a);
     }
     keys[base + e] = (uint32_t)(ty * gx + tx);
     vals[base + e] = (uint32_t)(s0 + lo) | (0xFu << ID_BITS);
@@ -556,8 +580,8 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
   const int ntiles = v.gx * v.gy;
   GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   if (P > 0 && N > 0) {
-    const size_t lds = (size_t)u.n * 2 * 256 * sizeof(float4);
-    const dim3 grid((unsigned)((P + 255) / 256));
+    const size_t lds = (size_t)u.n * 2 * DUPU_G * sizeof(float4);
+    const dim3 grid((unsigned)((P + DUPU_G - 1) / DUPU_G));
     switch (u.n) {
 #define GSLM_DUP_UNION(NS)                                                                                         \
   case NS:                                                                                                         \
@@ -573,7 +597,7 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
     }
     GSLM_LAUNCH_CHECK();
     bool alt = false;
-    int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, bb.hist, &alt, s, false, nullptr,
+    int st = radix_sort_pairs(bb.keys0, bb.vals0, bb.keys1, bb.vals1, N, bb.end_bit, um.hist, &alt, s, false, nullptr,
                               nullptr, um.m0, um.m1);
     if (st != GSLM_OK) return st;
     if ((alt ? bb.vals1 : bb.vals0) != bb.point_list || (alt ? um.m1 : um.m0) != um.sorted) {

@@ -45,17 +45,21 @@ constexpr int SORT_ITEMS_SMALL = GSLM_SORT_ITEMS_SMALL;
 constexpr int64_t SORT_FULL_BLOCKS = 1024;
 constexpr int RADIX = 256;
 
-inline int sort_items(int64_t n) {
-  return (n + SORT_TILE - 1) / SORT_TILE >= SORT_FULL_BLOCKS ? SORT_ITEMS : SORT_ITEMS_SMALL;
+// A sort that moves a payload array with the pairs always takes SORT_ITEMS_SMALL items per thread: at 16 the third
+// per-item register array pushes the scatter to 143 VGPRs (two waves per SIMD, 2x the time of the pair scatter).
+inline int sort_items(int64_t n, bool payload = false) {
+  return !payload && (n + SORT_TILE - 1) / SORT_TILE >= SORT_FULL_BLOCKS ? SORT_ITEMS : SORT_ITEMS_SMALL;
 }
-inline int64_t sort_blocks(int64_t n) {
-  const int64_t t = (int64_t)SORT_THREADS * sort_items(n);
+inline int64_t sort_blocks(int64_t n, bool payload = false) {
+  const int64_t t = (int64_t)SORT_THREADS * sort_items(n, payload);
   return (n + t - 1) / t;
 }
-inline size_t sort_hist_bytes(int64_t n) { return (size_t)RADIX * (size_t)sort_blocks(n) * 4 + 4 * RADIX; }
+inline size_t sort_hist_bytes(int64_t n, bool payload = false) {
+  return (size_t)RADIX * (size_t)sort_blocks(n, payload) * 4 + 4 * RADIX;
+}
 
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
-// ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n).
+// ping-pong buffers; *result_in_alt tells which pair holds the output.  hist: sort_hist_bytes(n, p0 != NULL).
 // last_gather (or NULL): the last pass writes last_gather[value] in place of each sorted key.
 // n_dev (or NULL): n is a capacity (grid and hist sized for it) and the kernels sort the first min(n, *n_dev) pairs.
 // p0 / p1 (or NULL): a second value array (p0 input, p1 its ping-pong partner) moved with the pairs; the result is

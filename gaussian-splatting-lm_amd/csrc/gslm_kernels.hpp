@@ -480,6 +480,7 @@ struct UnionMasks {
   uint32_t* m0;
   uint32_t* m1;
   uint32_t* sorted;
+  uint32_t* hist;  // the payload sort's histograms (sort_hist_bytes(N, true): more, smaller blocks than the pair sort)
 };
 size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* out);
 // all sets' blends + losses over a union list in one pass (render_fwd.hip, gslm_rasterize_loss_sets)

@@ -387,11 +387,11 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
                      const uint32_t* n_dev, uint32_t* p0, uint32_t* p1) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
-  const int nb = (int)sort_blocks(n);
-  const bool small = sort_items(n) != SORT_ITEMS;
+  const bool pay = p0 != nullptr;
+  const int nb = (int)sort_blocks(n, pay);
+  const bool small = sort_items(n, pay) != SORT_ITEMS;
   uint32_t* totals = hist + (size_t)RADIX * nb;
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1, *pi = p0, *po = p1;
-  const bool pay = p0 != nullptr;
   bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
   bool alt = false;
   // ceil(end_bit / 8) passes with the bits split evenly (13-bit tile ids: 7 + 6, not 8 + 5): fewer, longer
@@ -416,12 +416,8 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
     } else {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb, n_dev);
       hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
-      if (pay)
-        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
-                           shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)pi, po);
-      else
-        hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, false>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
-                           shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+      hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, false>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
+                         shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
     }
     first = false;
     GSLM_LAUNCH_CHECK();
