@@ -141,7 +141,10 @@ __device__ __forceinline__ bool band_x_extent(const QuadCull& q, float ya, float
   const float y0 = fmaxf(ya, -q.ydom), y1 = fminf(yb, q.ydom);
   if (!(y0 <= y1)) return false;
   const float yh = fminf(fmaxf(q.yr, y0), y1), yl = fminf(fmaxf(-q.yr, y0), y1);
-  const float sh = sqrtf(fmaxf(q.ta - q.det * yh * yh, 0.0f)), sl = sqrtf(fmaxf(q.ta - q.det * yl * yl, 0.0f));
+  // the hardware square root (v_sqrt_f32, within 1 ulp; sqrtf's correctly rounded expansion is ~4x the
+  // instructions, and this runs per (tile, Gaussian) pair): its error is far inside the 1e-4 widening below
+  const float sh = __builtin_amdgcn_sqrtf(fmaxf(q.ta - q.det * yh * yh, 0.0f));
+  const float sl = __builtin_amdgcn_sqrtf(fmaxf(q.ta - q.det * yl * yl, 0.0f));
   const float bh = q.b * yh, bl = q.b * yl;
   hi = (sh - bh) * q.ia;
   lo = -(sl + bl) * q.ia;

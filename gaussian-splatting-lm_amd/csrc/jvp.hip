@@ -267,8 +267,9 @@ __global__ __launch_bounds__(256) void k_render_matvec(ViewK v, const uint2* __r
                                                         const uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ weight, float4* __restrict__ contrib,
                                                         int write_tail) {
-  // 128-entry batches: 19.7 KB of LDS per block -> 8 blocks (VGPR-limited to 6 waves per SIMD) per CU,
-  // the occupancy this latency-bound pass needs
+  // 128-entry batches.  The LM instantiation (WITH_XY = false): 19.7 KB of LDS and 56 VGPRs -> 8 blocks per CU, 8
+  // waves per SIMD (hipcc -Rpass-analysis=kernel-resource-usage; profiles/r04/resource_usage.txt); the drop-in
+  // one (screen-position tangents): 23.8 KB, 64 VGPRs -> 6 blocks per CU
   constexpr int B = MATVEC_BATCH;
   __shared__ uint64_t s_bits[16];
   __shared__ int s_cnt[4];
