@@ -21,19 +21,21 @@ template <bool RAW, bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess(ViewK v, GaussK g, float4* __restrict__ rec,
                                                      uint32_t* __restrict__ depth_key,
                                                      uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
-                                                     uint32_t* __restrict__ clampw, int* __restrict__ radii_out) {
+                                                     uint32_t* __restrict__ clampw, int* __restrict__ radii_out,
+                                                     int lead) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];  // STAGE: [256 * rest_stride]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (STAGE) {
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
     const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
     const int64_t total = nv * g.rest_stride;  // floats; i0 * rest_stride * 4 B is 16-B aligned (i0 % 256 == 0)
-    const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+    const float* rows = g.rest - lead + i0 * g.rest_stride;  // stage_lead
+    const float4* src4 = reinterpret_cast<const float4*>(rows);
     float4* dst4 = reinterpret_cast<float4*>(s_sh);
     for (int64_t e = threadIdx.x; e < total / 4; e += blockDim.x) dst4[e] = src4[e];
-    for (int64_t e = (total / 4) * 4 + threadIdx.x; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+    for (int64_t e = (total / 4) * 4 + threadIdx.x; e < total; e += blockDim.x) s_sh[e] = rows[e];
     __syncthreads();
-    g.rest = s_sh;
+    g.rest = s_sh + lead;
     g.rest_base = i0;
   }
   if (i >= g.P) return;
@@ -81,7 +83,8 @@ template <bool RAW>
 __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float4* __restrict__ rec,
                                                          uint32_t* __restrict__ depth_key,
                                                          uint32_t* __restrict__ tiles, uint2* __restrict__ rect,
-                                                         uint32_t* __restrict__ clampw, int* __restrict__ radii_out) {
+                                                         uint32_t* __restrict__ clampw, int* __restrict__ radii_out,
+                                                         int lead) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];  // [256 * rest_stride]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
@@ -97,7 +100,8 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
   const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
   const int64_t total = nv * g.rest_stride;  // i0 * rest_stride * 4 B is 16-B aligned (i0 % 256 == 0)
   const int64_t n4 = total / 4;
-  const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+  const float* rows = g.rest - lead + i0 * g.rest_stride;  // stage_lead
+  const float4* src4 = reinterpret_cast<const float4*>(rows);
   float4* dst4 = reinterpret_cast<float4*>(s_sh);
   for (int64_t c = w; c * 64 < n4; c += 4) {
     const int64_t e = min(c * 64 + lane, n4 - 1);  // past the rows: re-read the last float4 (its slot is unused)
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
   // 4. the DMA landed (the barrier's vmcnt(0)); a row tail that is not a whole float4 (last block only) by plain loads
   __syncthreads();
   if (n4 * 4 < total) {
-    for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+    for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = rows[e];
     __syncthreads();
   }
   if (!live) return;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
   if (radii_out) radii_out[i] = 0;
   if (o.depth > 0.2f) depth_key[i] = __float_as_uint(o.depth);  // as k_preprocess: every Gaussian before the near plane
   if (!vis) return;
-  g.rest = s_sh;
+  g.rest = s_sh + lead;
   g.rest_base = i0;
   preprocess_color(v, g, i, in, o);
   const float4 r0 = make_float4(o.x, o.y, o.conic[0], o.conic[1]);
@@ -615,6 +619,7 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
 }
 
 // ------------------------------------------------------------------ launchers
+
 // k_preprocess_dma (default) or the register-staged k_preprocess: GSLM_PREPROCESS_STAGING=reg selects the latter
 // (an A/B switch; both write the bitwise same records)
 static const bool g_preprocess_dma = [] {
@@ -625,28 +630,30 @@ static const bool g_preprocess_dma = [] {
 int launch_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int* radii_out, hipStream_t s) {
   if (g.P == 0) return GSLM_OK;
   const int nb = (int)((g.P + 255) / 256);
-  // stage the SH rest through LDS when it is the contiguous [P, M-1, 3] leaf (raw GaussianModel tensors)
-  const bool stage = !g.colors && g.rest && g.M > 1 && g.rest_stride == 3 * (g.M - 1) &&
-                     ((uintptr_t)g.rest & 15u) == 0;
+  // stage the SH rows through LDS: the contiguous [P, M-1, 3] rest leaf (raw GaussianModel tensors, or the dc / rest
+  // pair of render(separate_sh=True)), or the rest inside upstream's [P, M, 3] features tensor (render()'s
+  // get_features: each rest row 3 floats past its dc at one 3M stride) -- whole rows staged from the dc slot
+  const int lead = stage_lead(g);
+  const bool stage = lead >= 0;
   const size_t lds = stage ? (size_t)256 * g.rest_stride * sizeof(float) : 0;
   if (g.raw && stage && g_preprocess_dma)
     hipLaunchKernelGGL((k_preprocess_dma<true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   else if (stage && g_preprocess_dma)
     hipLaunchKernelGGL((k_preprocess_dma<false>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   else if (g.raw && stage)
     hipLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   else if (g.raw)
     hipLaunchKernelGGL((k_preprocess<true, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   else if (stage)
     hipLaunchKernelGGL((k_preprocess<false, true>), dim3(nb), dim3(256), lds, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   else
     hipLaunchKernelGGL((k_preprocess<false, false>), dim3(nb), dim3(256), 0, s, v, g, gb.rec, gb.depth_key, gb.tiles,
-                       gb.rect, gb.clampw, radii_out);
+                       gb.rect, gb.clampw, radii_out, lead);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

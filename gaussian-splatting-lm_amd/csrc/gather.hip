@@ -186,6 +186,8 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
   const unsigned nb = (unsigned)((g.P + 255) / 256);
   const size_t sh_lds = sh_stage_floats<true>(g.M) * sizeof(float);
   const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
+  // (staging the primal SH rows here as k_preprocess_jvp does measured 221 -> 229 us at 1M: the 48 KB of LDS cost
+  // more occupancy than the strided reads; profiles/r04/ab/dropin_staging)
   const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
   if (g.raw)
     hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,

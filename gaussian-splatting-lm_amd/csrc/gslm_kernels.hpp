@@ -84,6 +84,34 @@ __device__ __forceinline__ float alpha_threshold(float op_eff) {
   return f;
 }
 
+// How the preprocess kernels may stage the block's SH rows in LDS: -1 not at all (colours given, degree 0, an odd
+// layout); else the floats between a staged row's start and its rest -- 0 for the contiguous rest leaf, 3 for the rest
+// inside a [P, M, 3] features tensor (rows staged from the dc slot).  The staged span must start 16-B aligned.
+inline int stage_lead(const GaussK& g) {
+  if (g.colors || !g.rest || g.M <= 1) return -1;
+  int lead = -1;
+  if (g.rest_stride == 3 * (g.M - 1)) lead = 0;
+  else if (g.dc && g.rest == g.dc + 3 && g.dc_stride == g.rest_stride && g.rest_stride == 3 * g.M) lead = 3;
+  if (lead < 0 || ((uintptr_t)(g.rest - lead) & 15u) != 0) return -1;
+  return lead;
+}
+
+// Copies the block's [nv][rest_stride] SH rows (from `lead` floats before g.rest, stage_lead) to LDS with coalesced
+// 16-B loads and points g.rest at the copy.  Block-uniform; ends with a barrier.
+__device__ __forceinline__ void stage_sh_rows(GaussK& g, int lead, float* s_rows) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+  const int64_t total = nv > 0 ? nv * g.rest_stride : 0;  // i0 * rest_stride * 4 B is 16-B aligned (i0 % 256 == 0)
+  const float* rows = g.rest - lead + i0 * g.rest_stride;
+  const float4* src4 = reinterpret_cast<const float4*>(rows);
+  float4* dst4 = reinterpret_cast<float4*>(s_rows);
+  for (int64_t e = threadIdx.x; e < total / 4; e += blockDim.x) dst4[e] = src4[e];
+  for (int64_t e = (total / 4) * 4 + threadIdx.x; e < total; e += blockDim.x) s_rows[e] = rows[e];
+  __syncthreads();
+  g.rest = s_rows + lead;
+  g.rest_base = i0;
+}
+
 // Per-Gaussian part of the quadrant test (k_duplicate prepares it once and tests every tile of the
 // rect).  mode: 0 = reaches no pixel, 1 = treat every quadrant as reachable, 2 = test.
 //

@@ -105,10 +105,16 @@ template <bool RAW, bool XPBY>
 __global__ __launch_bounds__(256) void k_preprocess_jvp(ViewK v, GaussK g, GaussK t, const float* __restrict__ m2t,
                                                          const uint32_t* __restrict__ clampw,
                                                          const uint32_t* __restrict__ tiles,
-                                                         float4* __restrict__ trec, XpbyK xp, int compact) {
-  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]
+                                                         float4* __restrict__ trec, XpbyK xp, int compact,
+                                                         int lead) {
+  extern __shared__ __attribute__((aligned(16))) float s_rest[];  // XPBY: [256 * 3(M-1)]; lead >= 0: [256 * rest_stride]
   if (cg_stopped(v)) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!XPBY && lead >= 0) {
+    // the drop-in JVP: the block's primal SH rows through LDS (per-thread reads at a 3M-float stride touch a line
+    // per lane per load; stage_lead)
+    stage_sh_rows(g, lead, s_rest);
+  }
   if (XPBY) {
     // the direction this kernel reads is the updated one: each thread reads back only its own
     // Gaussian's elements, all written by this block before the barrier; its SH-rest tangent (the
@@ -143,17 +149,19 @@ int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const f
     const size_t lds = (size_t)256 * xp->w[2] * sizeof(float);
     if (g.raw)
       hipLaunchKernelGGL((k_preprocess_jvp<true, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
-                         sb.trec, x, compact ? 1 : 0);
+                         sb.trec, x, compact ? 1 : 0, -1);
     else
       hipLaunchKernelGGL((k_preprocess_jvp<false, true>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
-                         sb.trec, x, compact ? 1 : 0);
+                         sb.trec, x, compact ? 1 : 0, -1);
   } else {
+    const int lead = g.P > 0 ? stage_lead(g) : -1;
+    const size_t lds = lead >= 0 ? (size_t)256 * g.rest_stride * sizeof(float) : 0;
     if (g.raw)
-      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.clampw, gb.tiles,
-                         sb.trec, x, compact ? 1 : 0);
+      hipLaunchKernelGGL((k_preprocess_jvp<true, false>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
+                         sb.trec, x, compact ? 1 : 0, lead);
     else
-      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), 0, s, v, g, t, m2t, gb.clampw, gb.tiles,
-                         sb.trec, x, compact ? 1 : 0);
+      hipLaunchKernelGGL((k_preprocess_jvp<false, false>), dim3(nb), dim3(256), lds, s, v, g, t, m2t, gb.clampw, gb.tiles,
+                         sb.trec, x, compact ? 1 : 0, lead);
   }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
