@@ -45,10 +45,12 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
   const uint32_t* pl = point_list + range.x;
   float4* s = s_rec[q];
 
-  // A stopped lane (or one outside the image) carries T = 0, and Tstop its transmittance at the stop: every visit
-  // then runs the same per-lane arithmetic with no boolean lane state across iterations (each one would cost a
-  // few scalar mask instructions per visit; with them the loop was bound by its scalar instructions, not VALU).
-  float T = inside ? 1.0f : 0.0f, Tstop = 0.0f;
+  // A stopped lane (or one outside the image) carries T <= 0: minus its transmittance at the stop, which a live lane
+  // (T >= 1e-4) never is.  Every visit then runs the same per-lane arithmetic with no boolean lane state across
+  // iterations (each one would cost a few scalar mask instructions per visit; with them the loop was bound by its
+  // scalar instructions, not VALU): a stopped lane's test_T = T (1 - u) <= 0 stops it again, with weight 0, and
+  // -|T| keeps T -- one select with source modifiers, where a separate stop-transmittance register cost two VALU.
+  float T = inside ? 1.0f : 0.0f;
   uint32_t last = 0;
   float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
   uint64_t dmask = __builtin_amdgcn_ballot_w64(!inside);  // lanes stopped (or outside the image), wave-uniform
@@ -88,15 +90,14 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       C1 += b.w * wt;
       C2 += cc.x * wt;
       if (MODE == FWD_FULL) Dp += cc.y * wt;
-      Tstop = stop ? Tstop + T : Tstop;
-      T = stop ? 0.0f : test_T;
+      T = stop ? -fabsf(T) : test_T;
       if (MODE != FWD_LOSS) last = wt > 0.0f ? (uint32_t)(base + j + 1) : last;  // blended: 1-based list position
       dmask |= __builtin_amdgcn_ballot_w64(stop);  // the stop compare's lane mask, no VGPR round trip
       if (dmask == ~0ull) break;
     }
     wave_lds_sync();
   }
-  T = T > 0.0f ? T : Tstop;  // the transmittance the reference keeps: at the stop, else after the last Gaussian
+  T = T > 0.0f ? T : -T;  // the transmittance the reference keeps: at the stop, else after the last Gaussian
   const int64_t pid = (int64_t)py * v.W + px;
   const int64_t HW = (int64_t)v.H * v.W;
   if constexpr (MODE == FWD_LOSS) {
@@ -152,13 +153,12 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
   const uint32_t* pl = point_list + range.x;
   const uint32_t* am = amask + range.x;
   float4* s = s_rec[q];
-  float T[NS], Tstop[NS], C0[NS], C1[NS], C2[NS];
+  float T[NS], C0[NS], C1[NS], C2[NS];  // T: k_render_fwd_wave's stopped-lane encoding (-|T| at the stop)
   uint64_t dmask[NS];
   const uint64_t out0 = __builtin_amdgcn_ballot_w64(!inside);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
     T[a] = inside ? 1.0f : 0.0f;
-    Tstop[a] = 0.0f;
     C0[a] = C1[a] = C2[a] = 0.f;
     dmask[a] = out0;
   }
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
           rc = r[2];
         }
       }
-      float Ta = T[a], Tsa = Tstop[a], c0 = C0[a], c1 = C1[a], c2 = C2[a];
+      float Ta = T[a], c0 = C0[a], c1 = C1[a], c2 = C2[a];
       uint64_t dm = dmask[a];
       while (hb) {
         const int j = (int)__builtin_ctzll(hb);
@@ -218,13 +218,11 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
         c0 += y.z * wt;
         c1 += y.w * wt;
         c2 += z.x * wt;
-        Tsa = stop ? Tsa + Ta : Tsa;
-        Ta = stop ? 0.0f : test_T;
+        Ta = stop ? -fabsf(Ta) : test_T;
         dm |= __builtin_amdgcn_ballot_w64(stop);
         if (dm == ~0ull) break;
       }
       T[a] = Ta;
-      Tstop[a] = Tsa;
       C0[a] = c0;
       C1[a] = c1;
       C2[a] = c2;
@@ -246,7 +244,7 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
   for (int a = 0; a < NS; ++a) {
     double acc = 0.0;
     if (inside) {
-      const float Tf = T[a] > 0.0f ? T[a] : Tstop[a];
+      const float Tf = T[a] > 0.0f ? T[a] : -T[a];
       const float R[3] = {C0[a] + Tf * v.bg[0], C1[a] + Tf * v.bg[1], C2[a] + Tf * v.bg[2]};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
