@@ -86,10 +86,11 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       // a live lane has T >= 1e-4, so with u = 0 it never stops here; a stopped lane (T = 0) re-stops harmlessly
       const bool stop = test_T < 0.0001f;
       const float wt = stop ? 0.0f : u * T;
-      C0 += b.z * wt;
-      C1 += b.w * wt;
-      C2 += cc.x * wt;
-      if (MODE == FWD_FULL) Dp += cc.y * wt;
+      // the colour sums decide nothing (the stop and skip tests above are upstream's roundings): one FMA each
+      C0 = __builtin_fmaf(b.z, wt, C0);
+      C1 = __builtin_fmaf(b.w, wt, C1);
+      C2 = __builtin_fmaf(cc.x, wt, C2);
+      if (MODE == FWD_FULL) Dp = __builtin_fmaf(cc.y, wt, Dp);
       T = stop ? -fabsf(T) : test_T;
       if (MODE != FWD_LOSS) last = wt > 0.0f ? (uint32_t)(base + j + 1) : last;  // blended: 1-based list position
       dmask |= __builtin_amdgcn_ballot_w64(stop);  // the stop compare's lane mask, no VGPR round trip
@@ -215,9 +216,9 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
         const float test_T = Ta * (1.0f - u);
         const bool stop = test_T < 0.0001f;
         const float wt = stop ? 0.0f : u * Ta;
-        c0 += y.z * wt;
-        c1 += y.w * wt;
-        c2 += z.x * wt;
+        c0 = __builtin_fmaf(y.z, wt, c0);  // k_render_fwd_wave's colour FMAs
+        c1 = __builtin_fmaf(y.w, wt, c1);
+        c2 = __builtin_fmaf(z.x, wt, c2);
         Ta = stop ? -fabsf(Ta) : test_T;
         dm |= __builtin_amdgcn_ballot_w64(stop);
         if (dm == ~0ull) break;
