@@ -626,9 +626,12 @@ def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True, 
     saved = [t.detach().clone() for t in model.params()]
 
     def restore():
+        # xyz is masked (train_jvp.py:221-227): lm_step never writes it, and copying it anyway would bump its version
+        # and drop the validation views' cached depth orders, which in train_jvp.py's loop live across LM steps
         with torch.no_grad():
             for t, s0 in zip(model.params(), saved):
-                t.copy_(s0)
+                if t is not model._xyz:
+                    t.copy_(s0)
 
     restart = iters if restart is None else restart
     out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart)  # warm-up (workspaces, clocks)

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
 // hits are visited, so a round waits on two dependent loads (entries, set 0's records) instead of two per set.
 // Every set's visits and their order are the single-set kernel's: the same losses, bitwise.
 template <int NS>
-__global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8 : 1))) void k_render_loss_sets(ViewK v, const uint2* __restrict__ ranges,
                                                            const uint32_t* __restrict__ tile_order,
                                                            const uint32_t* __restrict__ point_list,
                                                            const uint32_t* __restrict__ amask, SetRecsK sr,
@@ -231,12 +231,12 @@ __global__ __launch_bounds__(256) void k_render_loss_sets(ViewK v, const uint2* 
       wave_lds_sync();  // this set's hits read before the next set's are staged
     }
   }
-  const int64_t pid = (int64_t)py * v.W + px;
   const int64_t HW = (int64_t)v.H * v.W;
   __shared__ double s_sum[NS][4];
   float gtc[3] = {0.f, 0.f, 0.f};
   float mv = 1.0f;
   if (inside) {
+    const int64_t pid = (int64_t)(int)pyf * v.W + (int)pxf;  // from the loop's live pixel centre, not a kept index
     mv = mask ? mask[pid] : 1.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) gtc[c] = gt[c * HW + pid];
