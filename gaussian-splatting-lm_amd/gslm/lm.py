@@ -821,12 +821,11 @@ class LossEvaluator:
         self.uslots = [[dict(geoms=[], ugeom=None) for _ in range(self.batch)] for _ in range(2)]
         self.ubins = [None] * self.batch
         self.sets_scratch = [None] * self.batch
-        # the six points' blends: one pass for all sets over each union list (gslm_rasterize_loss_sets), or one pass per
-        # set (gslm_rasterize_loss_slot; GSLM_LOSS_SETS=0) -- the same losses bitwise.  All sets is the default since
-        # its visit lost the stop-transmittance registers (64 VGPRs, 8 waves per SIMD): 69.8 against 74.8 ms for the six
-        # points over 50 views (profiles/r04/ab/all_sets_default/; at 74 VGPRs it had been the slower one beside the
-        # other streams' work)
-        self.loss_sets = os.environ.get("GSLM_LOSS_SETS", "1") != "0"
+        # the six points' blends: one pass per set over each union list (gslm_rasterize_loss_slot), or one pass for all
+        # sets (gslm_rasterize_loss_sets; GSLM_LOSS_SETS=1) -- the same losses bitwise.  Per set is the default: the
+        # all-sets pass wins when evaluate_points runs back to back (69.8 against 74.8 ms for the six points over 50
+        # views) but loses inside lm_step (LM step 98.3 against 95.5 ms, same box; profiles/r04/ab/all_sets_default/)
+        self.loss_sets = os.environ.get("GSLM_LOSS_SETS", "0") == "1"
         self.union_counts = []
 
     def _slot(self, k, P):
