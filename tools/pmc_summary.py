@@ -48,7 +48,8 @@ def main(out_dir):
         with open(sys.argv[2], "w") as f:
             json.dump({"kernel": mv[0], "P": 1000000, "width": 1920, "height": 1080,
                        "command": "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) -- "
-                                  "python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --forward-steps 8",
+                                  "python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --forward-steps 8 --no-side",
+                       "round": os.environ.get("GSLM_PMC_ROUND", ""),
                        "fetch_bytes_per_launch_raw": r["fetch_bytes_per_launch_raw"],
                        "write_bytes_per_launch": r["write_bytes_per_launch"],
                        "hbm_bytes_per_launch": r["fetch_bytes_per_launch_x2"] + r["write_bytes_per_launch"],
