@@ -16,6 +16,7 @@ import torch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--P", type=int, default=1_000_000)
+ap.add_argument("--copy-xyz", action="store_true", help="restore xyz too between steps (drops the cached depth orders)")
 a = ap.parse_args()
 from gslm.cameras import orbit_cameras  # noqa: E402
 from gslm.lm import LMProblem, lm_step  # noqa: E402
@@ -46,11 +47,11 @@ saved = [t.detach().clone() for t in model.params()]
 def restore():
     with torch.no_grad():
         for t, s0 in zip(model.params(), saved):
-            if t is not model._xyz:
+            if a.copy_xyz or t is not model._xyz:
                 t.copy_(s0)
 
 
-out = {"untimed_ms": [], "timed": []}
+out = {"copy_xyz": a.copy_xyz, "untimed_ms": [], "timed": []}
 lm_step(model, cams, val, bg, max_iter=10, restart_iter=10)
 restore()
 for _ in range(a.reps):
