@@ -475,9 +475,13 @@ __global__ __launch_bounds__(256) void k_union_rect(int64_t P, UnionSets u, uint
 // and the set's rect -- and every element evaluates quad_mask on it: the bits k_duplicate writes for that set's own
 // list.  (Preparing per element was 6 square roots and 4 divisions per set and entry: 252 us per 1080p view at 1M,
 // 5x the plain k_duplicate.)  The centre is the same in every set that keeps the Gaussian (the points share xyz and
-// the view), so its copy in s_gxy is written by each such set with the same bits.  Half-size blocks keep the
-// staging at NS * 5 KB of LDS (dynamic: NS * 2 * DUPU_G float4).
-constexpr int DUPU_G = 128;
+// the view), so its copy in s_gxy is written by each such set with the same bits.  Quarter-size blocks keep the
+// staging at NS * 2.5 KB of LDS (dynamic: NS * 2 * DUPU_G float4); DUPU_SPLIT threads share a Gaussian's sets.
+#ifndef GSLM_DUPU_G
+#define GSLM_DUPU_G 64  // 64: 15 KB of staging at six sets, 8 blocks per CU (union binning 0.290 -> 0.272 ms against 128)
+#endif
+constexpr int DUPU_G = GSLM_DUPU_G;
+constexpr int DUPU_SPLIT = 256 / DUPU_G;  // threads per Gaussian in the staging
 template <int NS>
 __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ offsets,
                                                           uint32_t N, const uint2* __restrict__ urect, UnionSets u,
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
   __shared__ float2 s_gxy[DUPU_G];
   __shared__ uint32_t s_off[DUPU_G + 1];
   __shared__ uint32_t s_rc[DUPU_G][3];  // x0, y0, width of the union rect
-  const int tid = threadIdx.x, gi = tid & (DUPU_G - 1), half = tid >> 7;
+  const int tid = threadIdx.x, gi = tid & (DUPU_G - 1), half = tid / DUPU_G;
   const int64_t s0 = (int64_t)blockIdx.x * DUPU_G, s = s0 + gi;
   const int64_t slast = min(s0 + DUPU_G - 1, P - 1);
   const uint32_t base = offsets[s0];
@@ -508,8 +512,8 @@ __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, cons
     }
     if (n) {
 #pragma unroll
-      for (int k = 0; k < (NS + 1) / 2; ++k) {
-        const int a = 2 * k + half;
+      for (int k = 0; k < (NS + DUPU_SPLIT - 1) / DUPU_SPLIT; ++k) {
+        const int a = DUPU_SPLIT * k + half;
         if (a >= NS) break;
         const float4* r = u.rec[a] + RECS * (size_t)s;
         const float4 r0 = r[0], r3 = r[3];
