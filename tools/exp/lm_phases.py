@@ -10,7 +10,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-splatting-lm_amd")]
+sys.path[:0] = [ROOT, os.environ.get("GSLM_PKG_DIR", os.path.join(ROOT, "gaussian-splatting-lm_amd"))]
 import torch  # noqa: E402
 
 ap = argparse.ArgumentParser()
