@@ -267,3 +267,54 @@ def test_fullsize_backward_whole_frame_100k():
     for k in ref:
         err = _rel_err(got[k], ref[k])
         assert err < 1e-4, f"grad {k}: rel err {err:.3e}"
+
+
+def test_fullsize_lm_matvec_whole_frame_100k():
+    """configs[1]'s fused LM product (J^T W J v, xyz masked, zero damping) with the per-pixel weights of the WHOLE
+    frame (no tile sample) against the oracle's forward-AD J v and autograd J^T over every tile (1e-4 of each group's
+    max)."""
+    from gslm.lm import LMProblem
+    name = "cfg1_100k_sh3_1080p"
+    model, cam = _scene(CONFIGS[name])
+    zero_damp = {k: 0.0 for k in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity",
+                                  "exposure")}
+    gm = synthetic_gaussians(CONFIGS[name], 3, seed=0, s0=0.005, device="cpu", n_cams=1).to(DEV)
+    cg = orbit_cameras(1, W, H, seed=1)[0].to(DEV)
+    prob = LMProblem(gm, [cg], torch.zeros(3), gts=[torch.zeros(3, H, W, device=DEV)],
+                     alpha_masks=[torch.ones(1, H, W, device=DEV)], damp=zero_damp)
+    prob.evaluate()
+    w = prob.weights[0].cpu()
+    gen = torch.Generator().manual_seed(3)
+    v = torch.randn(prob.layout.numel, generator=gen)
+    o = prob.layout.offsets
+    v[o["xyz"][0]:o["xyz"][1]] = 0
+    v[o["exposure"][0]:o["exposure"][1]] = 0
+    y = prob.matvec(v.to(DEV), prob.zeros()).cpu()
+    groups = ["features_dc", "features_rest", "scaling", "rotation", "opacity"]
+    leaves = {g: "_" + g for g in groups}
+    tang = {g: v[o[g][0]:o[g][1]].reshape(getattr(model, leaves[g]).shape) for g in groups}
+
+    def render():
+        st = oracle_settings(cam, 3)
+        pre = tr.preprocess(model.get_xyz, torch.zeros_like(model.get_xyz), model.get_opacity,
+                            model.get_features, None, model.get_scaling, model.get_rotation, None, st)
+        pl, _, rg = tr.binning(pre)
+        color, _, _, _ = tr.blend(pre, pl, rg, H, W, st.bg)
+        return color
+
+    with torch.no_grad(), fwAD.dual_level():
+        saved = {g: getattr(model, leaves[g]) for g in groups}
+        try:
+            for g in groups:
+                setattr(model, leaves[g], fwAD.make_dual(saved[g], tang[g]))
+            q = fwAD.unpack_dual(render()).tangent
+        finally:
+            for g in groups:
+                setattr(model, leaves[g], saved[g])
+    for g in groups:
+        getattr(model, leaves[g]).requires_grad_(True)
+    (render() * (2.0 * w * q)).sum().backward()
+    for g in groups:
+        err = _rel_err(y[o[g][0]:o[g][1]], getattr(model, leaves[g]).grad.reshape(-1))
+        assert err < 1e-4, f"group {g}: rel err {err:.3e}"
+    assert y[o["xyz"][0]:o["xyz"][1]].abs().max() == 0
