@@ -234,3 +234,16 @@ def _al(x):
 def _off(rec, keys):
     """Byte offset of the tile counts in the geometry layout (rec, depth_key, tiles, ...; 256-B aligned, api.hip)."""
     return _al(rec) + _al(keys)
+
+
+@pytest.mark.parametrize("P", [1, 5, 63, 65, 129])
+def test_evaluate_points_tiny_and_ragged(P):
+    """The union path at a handful of Gaussians (block tails of the 64-Gaussian duplicate blocks and the 8-item payload
+    sort, views where the union list is empty) equals the exact renders."""
+    from gslm.lm import LossEvaluator
+    m, cams = _scene(P=P, nviews=3, s0=0.05)
+    lay, s = _step(m, seed=7)
+    ev_x = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
+    ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
+    sets, exact, _, _ = _points(m, lay, s, ev_x)
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
