@@ -225,6 +225,24 @@ def main():
     t_cg = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = 1e3 * t_cg / args.steps
 
+    # the same K iterations with the reference's stopping tests each iteration (conjugate_gradient.py:88-117: delta,
+    # the residual monitor b^2 - <x, g> - <x, s>, the gamma tolerance), evaluated on the device (gslm_cg_monitor; the
+    # monitor's two dots fused into the update pass): what an iteration of train_jvp.py's CGLS costs in full.  The
+    # timed loop above skips only those scalar tests (its iterates are identical while no test fires).  Warm-up
+    # first: the monitor's kernels load on their first launch.
+    cgls_fused(prob, g, max_iter=max(args.warmup, 1), restart_iter=max(args.warmup, 1), check_every=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, info_chk = cgls_fused(prob, g, max_iter=args.steps, restart_iter=args.steps, check_every=True)
+    torch.cuda.synchronize()
+    barrier()
+    t_chk = max_over_ranks(time.perf_counter() - t0)
+    cg_checked = {"ms_per_step": 1e3 * t_chk / args.steps, "view_matvec_per_s": n_views * args.steps / t_chk,
+                  "iters_before_stop": info_chk["iters"], "stop": info_chk.get("stop"),
+                  "note": "the timed K iterations with the reference's stopping tests on the device each iteration "
+                          "(stop 0: none fired; a fired test leaves the later launches returning at once)"}
+
     # the same CG loop on the reference's full param-space layout (59 floats per Gaussian at SH 3), for
     # comparison when the projected SH-rest layout ran above
     cg_full = None
@@ -442,6 +460,7 @@ def main():
                        "views_total": n_views, "parallelism": f"views sharded x{world_size}",
                        "exchange": exchange, "sh_rest_projected": bool(sh_proj)},
             "cg_matvecs_per_s": args.steps / t_cg,
+            "cg_checked": cg_checked,
             "clock_settle": dict(settle, note="untimed CG calls before the warm-up and timed steps: the GPU clocks "
                                               "at their steady state, as in a running LM solve"),
             "raster_mpix_s": mpix,
