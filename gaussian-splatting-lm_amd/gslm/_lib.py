@@ -189,6 +189,15 @@ EXPORTS = {
     "gslm_damp_add": (ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                      ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p]),
+    "gslm_comm_id_bytes": (ctypes.c_int32, []),
+    "gslm_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "gslm_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(ctypes.c_void_p)]),
+    "gslm_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "gslm_allreduce_sum_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "gslm_allreduce_sum_f64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "gslm_alltoall": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_void_p]),
     "gslm_residual_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]),
     "gslm_lm_residual": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -42,12 +42,37 @@ def collectives_on(world_size):
     return world_size > 1 or os.environ.get("GSLM_FORCE_COLLECTIVES") == "1"
 
 
+_NATIVE = {}
+
+
+def native_comm(group=None, device=None):
+    """The GSLM_COMM=native communicator of `group` (gslm.comm.NativeComm over the C-ABI RCCL entry points), made on
+    first use -- a collective call, reached in the same program order on every rank -- or None (torch.distributed)."""
+    from gslm import comm
+    if not comm.enabled():
+        return None
+    key = id(group)
+    if key not in _NATIVE:
+        _NATIVE[key] = comm.NativeComm(group, device)
+    return _NATIVE[key]
+
+
+def _device_allreduce(t, group):
+    """In-place sum over the ranks: the native communicator for device tensors under GSLM_COMM=native, otherwise
+    torch.distributed (host-staged under gloo)."""
+    nc = native_comm(group, t.device) if t.is_cuda else None
+    if nc is not None:
+        nc.all_reduce_(t)
+    else:
+        _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group), t)
+
+
 def allreduce_loss(t, group=None):
     """Sum a device (or host) double over the ranks in place: the multi-GPU line search's validation loss, one
     8-byte all-reduce per evaluation (every rank gets the bitwise same sum, so every rank takes the same
     line-search decisions)."""
     if collectives_on(world()[1]):
-        _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group), t.view(1))
+        _device_allreduce(t.view(1), group)
     return t
 
 
@@ -121,7 +146,7 @@ class ShardedOperator:
 
     def _allreduce(self, t):
         if collectives_on(self.world_size):
-            _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
+            _device_allreduce(t, self.group)
         return t
 
     def evaluate(self):
@@ -295,12 +320,19 @@ class GaussianShardedOperator:
     # ------------------------------------------------------------------ collectives
     def _allreduce(self, t):
         if collectives_on(self.world_size) and not self._emulate:
-            _staged(lambda x: dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group), t)
+            _device_allreduce(t, self.group)
         return t
+
+    def _native(self, t):
+        return native_comm(self.group, t.device) if t.is_cuda else None
 
     def _all_to_all(self, out, inp):
         if not collectives_on(self.world_size) or self._emulate:
             out.copy_(inp)
+            return
+        nc = self._native(out)
+        if nc is not None:
+            nc.all_to_all(out, inp)
             return
         _staged(lambda o, i: dist.all_to_all_single(o, i, group=self.group), out, inp)
 
@@ -310,11 +342,16 @@ class GaussianShardedOperator:
         was issued; Work.wait() orders the compute stream after it).  gloo stages through the host: synchronous."""
         if self._emulate or not collectives_on(self.world_size) or os.environ.get("GSLM_OVERLAP", "1") == "0":
             return False
-        return dist.get_backend(self.group) == "nccl"
+        from gslm import comm
+        return dist.get_backend(self.group) == "nccl" or (comm.enabled() and
+                                                         torch.device(self.device).type == "cuda")
 
     def _all_to_all_async(self, out, inp):
         """all_to_all_single issued without waiting: the Work to wait on, or None once done (synchronous paths)."""
         if self._overlap():
+            nc = self._native(out)
+            if nc is not None:
+                return nc.all_to_all_async(out, inp)
             return dist.all_to_all_single(out, inp, group=self.group, async_op=True)
         self._all_to_all(out, inp)
         return None

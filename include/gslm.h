@@ -430,6 +430,26 @@ int gslm_dot_finalize(const void* partials, int32_t np, double* out_dev, void* s
 int gslm_damp_add(int64_t n, const float* x, const int64_t* group_bounds, const double* group_damp,
                   int32_t ngroups, float* y, void* stream);
 
+/* ---- RCCL collectives over xGMI, communicator handle passed in (SURVEY 8(b) "gslm_allreduce*", 8(e)) ----
+ * The reference has no multi-GPU code (its LinearSolverFunctions renders a view batch serially on one GPU,
+ * solver/solver_functions.py:88-93,110-121); these replace the all-reduce of J^T r / J^T J v and of the CG scalars
+ * that SURVEY 8(e) adds, and carry the Gaussian-sharded exchange's all-to-alls, for a host that does not go through
+ * torch.distributed (gslm.parallel uses them with GSLM_COMM=native; its default is torch.distributed's "nccl"
+ * backend, the same RCCL).  One rank calls gslm_comm_unique_id and the host broadcasts the gslm_comm_id_bytes()
+ * bytes; every rank then calls gslm_comm_init with its HIP device current (blocks until all ranks joined).  The
+ * collectives are enqueued on `stream` (RCCL stream semantics: ordered after the kernels enqueued on it before, and
+ * before those after) and never synchronise the host.  librccl is loaded on the first call (GSLM_ERR_HIP if absent). */
+int32_t gslm_comm_id_bytes(void);
+int gslm_comm_unique_id(void* id_out);
+int gslm_comm_init(const void* id, int32_t nranks, int32_t rank, void** comm_out);
+int gslm_comm_destroy(void* comm);
+/* in-place sums over the ranks: param-space partial products (f32), CG scalars / losses (f64) */
+int gslm_allreduce_sum_f32(void* comm, float* buf, int64_t n, void* stream);
+int gslm_allreduce_sum_f64(void* comm, double* buf, int64_t n, void* stream);
+/* recv[r * bytes_per_rank ...] = rank r's send[rank * bytes_per_rank ...] (the Gaussian-sharded exchange's records
+ * and screen sums, gslm_tangent_views / GSLM_STAGE_SCREEN) */
+int gslm_alltoall(void* comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream);
+
 /* ---- LM residual epilogue of one view (replaces the render clamp
  * gaussian_renderer/batch_render.py:118 + compute_batch_loss_block, solver/batch_training_loss.py:10-17,
  * 56-67, disable_ssim=True, and loss_scalar, solver/loss_image_state.py:16-19) ----

@@ -56,6 +56,33 @@ def main():
             del os.environ["GSLM_OVERLAP"]
             out["exchanges"][mode]["pipelined_bitwise"] = bool(torch.equal(res[0][0], res[1][0]) and
                                                                torch.equal(res[0][1], res[1][1]))
+            # the same product and iterates with every collective through the C-ABI RCCL communicator
+            # (GSLM_COMM=native: gslm_alltoall / gslm_allreduce_sum_*, pipelined on a side stream)
+            os.environ["GSLM_COMM"] = "native"
+            y = op.matvec(vs, op.zeros())
+            x, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=True)
+            torch.cuda.synchronize()
+            del os.environ["GSLM_COMM"]
+            x_t, _ = cgls_fused(op, g, max_iter=3, restart_iter=3, check_every=True)
+            torch.cuda.synchronize()
+            from gslm.parallel import _NATIVE
+            out["native"] = {"comm_made": len(_NATIVE) > 0, "y_bitwise": bool(torch.equal(y, res[0][0])),
+                             "x_bitwise": bool(torch.equal(x, x_t))}
+    # the C-ABI collectives on their own (one rank): sums and the all-to-all are identities / copies
+    from gslm.comm import NativeComm
+    nc = NativeComm(device="cuda")
+    a = torch.randn(1000, device="cuda")
+    a0 = a.clone()
+    nc.all_reduce_(a)
+    d64 = torch.randn(3, dtype=torch.float64, device="cuda")
+    d0 = d64.clone()
+    nc.all_reduce_(d64)
+    src = torch.arange(4096, dtype=torch.int32, device="cuda")
+    dst = torch.zeros_like(src)
+    nc.all_to_all_async(dst, src).wait()
+    torch.cuda.synchronize()
+    out["native"]["primitives"] = bool(torch.equal(a, a0) and torch.equal(d64, d0) and torch.equal(dst, src))
+    nc.close()
     # the whole LM step (train_jvp.py:237-279) on the sharded path: Gaussian-sharded CG + all-reduced line search
     import numpy as np
     from gslm.lm import lm_step

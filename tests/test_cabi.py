@@ -221,3 +221,23 @@ def test_no_product_kernel_uses_scratch(tmp_path):
     sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
     assert len(names) == len(sizes) and len(names) > 50
     assert [n for n, s in zip(names, sizes) if s] == []
+
+
+def test_comm_entry_points_check_arguments():
+    """The C-ABI RCCL communicator (gslm_comm_*, gslm_allreduce_sum_*, gslm_alltoall): the id size, and NULL handles /
+    bad ranks refused with GSLM_ERR_INVALID before RCCL is touched (no GPU here; tests/test_gpu_rccl.py runs them)."""
+    import ctypes as C
+    from gslm import _lib
+    lib = _lib.lib
+    assert lib.gslm_comm_id_bytes() == 128
+    h = C.c_void_p()
+    buf = (C.c_uint8 * 128)()
+    assert lib.gslm_comm_init(None, 1, 0, C.byref(h)) == -1
+    assert lib.gslm_comm_init(C.addressof(buf), 2, 2, C.byref(h)) == -1
+    assert lib.gslm_comm_init(C.addressof(buf), 0, 0, C.byref(h)) == -1
+    assert lib.gslm_comm_unique_id(None) == -1
+    assert lib.gslm_allreduce_sum_f32(None, None, 4, None) == -1
+    assert lib.gslm_allreduce_sum_f64(None, None, 4, None) == -1
+    assert lib.gslm_alltoall(None, None, None, 16, None) == -1
+    assert b"NULL" in lib.gslm_last_error()
+    assert lib.gslm_comm_destroy(None) == 0

@@ -33,6 +33,10 @@ def test_exchanges_through_rccl_one_rank():
     # two views per rank: the product ran pipelined (async all-to-alls per view group), bitwise the synchronous one
     assert res["exchanges"]["gaussian"]["pipelined"], res["exchanges"]["gaussian"]
     assert res["exchanges"]["gaussian"]["pipelined_bitwise"], res["exchanges"]["gaussian"]
+    # the C-ABI RCCL communicator (gslm_comm_*, GSLM_COMM=native) gives the torch.distributed path's product and
+    # CG iterates bitwise, and its collectives alone are identities at one rank
+    nat = res["native"]
+    assert nat["comm_made"] and nat["y_bitwise"] and nat["x_bitwise"] and nat["primitives"], nat
     lm = res["lm_step"]  # the sharded LM step through RCCL against the reference's (lm_step_golden.npz)
     assert lm["ranks"] == 1 and lm["best_alpha"] == lm["best_alpha_ref"], lm
     assert lm["step_rel"] <= 1e-4 and lm["final_rel"] <= 1e-4, lm
