@@ -3,8 +3,8 @@
 // The multi-GPU LM product (gslm.parallel) moves its data with torch.distributed, whose "nccl" backend is RCCL; a
 // host without torch drives the same exchanges through these entry points instead: a communicator made from a
 // unique id that one rank creates and the host broadcasts (any channel), then in-place sum all-reduces of the CG
-// scalars (f64) and of param-space partial products J^T r / J^T W J v (f32), and the all-to-all of the
-// Gaussian-sharded exchange.  Every call is enqueued on the caller's stream and returns at once (RCCL's own
+// scalars (f64) and of param-space partial products J^T r / J^T W J v (f32), the all-to-all of the
+// Gaussian-sharded exchange and the all-gather of the screen exchange.  Every call is enqueued on the caller's stream and returns at once (RCCL's own
 // stream semantics); the caller orders its kernels around it with the stream, as with any other launch.
 //
 // librccl is opened at the first communicator call (dlopen), not linked: the library loads and its compute entry
@@ -32,6 +32,7 @@ struct Rccl {
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
   decltype(&ncclAllReduce) AllReduce = nullptr;
   decltype(&ncclAllToAll) AllToAll = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
 };
 
@@ -49,9 +50,11 @@ const Rccl* rccl() {
     r.CommDestroy = reinterpret_cast<decltype(r.CommDestroy)>(dlsym(r.so, "ncclCommDestroy"));
     r.AllReduce = reinterpret_cast<decltype(r.AllReduce)>(dlsym(r.so, "ncclAllReduce"));
     r.AllToAll = reinterpret_cast<decltype(r.AllToAll)>(dlsym(r.so, "ncclAllToAll"));
+    r.AllGather = reinterpret_cast<decltype(r.AllGather)>(dlsym(r.so, "ncclAllGather"));
     r.GetErrorString = reinterpret_cast<decltype(r.GetErrorString)>(dlsym(r.so, "ncclGetErrorString"));
   });
-  if (!r.so || !r.GetUniqueId || !r.CommInitRank || !r.CommDestroy || !r.AllReduce || !r.AllToAll) {
+  if (!r.so || !r.GetUniqueId || !r.CommInitRank || !r.CommDestroy || !r.AllReduce || !r.AllToAll ||
+      !r.AllGather) {
     set_error("RCCL unavailable: librccl.so.1 not found or missing an entry point");
     return nullptr;
   }
@@ -150,6 +153,19 @@ int gslm_alltoall(void* comm, const void* send, void* recv, int64_t bytes_per_ra
   Comm* cm = static_cast<Comm*>(comm);
   return rccl_status(r, r->AllToAll(send, recv, (size_t)bytes_per_rank, ncclInt8, cm->c, (hipStream_t)stream),
                      "ncclAllToAll");
+}
+
+int gslm_allgather(void* comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream) {
+  if (!comm || bytes_per_rank < 0 || (bytes_per_rank > 0 && (!send || !recv))) {
+    set_error("allgather: NULL comm / buffers or negative size");
+    return GSLM_ERR_INVALID;
+  }
+  if (bytes_per_rank == 0) return GSLM_OK;
+  const Rccl* r = rccl();
+  if (!r) return GSLM_ERR_HIP;
+  Comm* cm = static_cast<Comm*>(comm);
+  return rccl_status(r, r->AllGather(send, recv, (size_t)bytes_per_rank, ncclInt8, cm->c, (hipStream_t)stream),
+                     "ncclAllGather");
 }
 
 }  // extern "C"

@@ -1,13 +1,15 @@
-"""Native RCCL communicator over the C ABI (gslm_comm_*, gslm_allreduce_sum_*, gslm_alltoall; csrc/comm.hip).
+"""Native RCCL communicator over the C ABI (gslm_comm_*, gslm_allreduce_sum_*, gslm_alltoall, gslm_allgather;
+csrc/comm.hip).
 
 gslm.parallel moves the multi-GPU LM product's data with torch.distributed ("nccl" = RCCL on ROCm) by default;
 with GSLM_COMM=native its device collectives go through this communicator instead -- the C-ABI collectives a host
 without torch would bind (SURVEY §8(b) "gslm_allreduce*", comm handle passed in).  torch.distributed is used once,
 to broadcast rank 0's RCCL unique id (the bootstrap any host needs some channel for).
 
-Semantics match the torch calls they replace: in-place sum all-reduce, all_to_all_single over equal dim-0 blocks,
-enqueued on the caller's current stream.  `all_to_all_async` issues the collective on a side stream ordered after
-the current stream's work and returns a handle whose wait() orders the current stream after it (Work.wait()).
+Semantics match the torch calls they replace (in-place sum all-reduce, all_to_all_single over equal dim-0 blocks,
+all_gather_into_tensor), enqueued on the caller's current stream.  `all_to_all_async` issues the collective on a
+side stream ordered after the current stream's work and returns a handle whose wait() orders the current stream
+after it (Work.wait()).
 """
 import ctypes
 import os
@@ -90,6 +92,16 @@ class NativeComm:
         s = stream.cuda_stream if stream is not None else _lib.stream_handle(out.device)
         check(lib.gslm_alltoall(self.handle, inp.data_ptr(), out.data_ptr(), nbytes // self.world_size, s),
               "gslm_alltoall")
+
+    def all_gather(self, out, inp):
+        """out's r-th dim-0 block <- rank r's inp (torch's all_gather_into_tensor)."""
+        if not (out.is_cuda and inp.is_cuda and out.is_contiguous() and inp.is_contiguous()):
+            raise ValueError("NativeComm.all_gather: contiguous device tensors")
+        nbytes = inp.numel() * inp.element_size()
+        if out.numel() * out.element_size() != nbytes * self.world_size:
+            raise ValueError("NativeComm.all_gather: out must hold world_size copies of inp")
+        check(lib.gslm_allgather(self.handle, inp.data_ptr(), out.data_ptr(), nbytes, _lib.stream_handle(out.device)),
+              "gslm_allgather")
 
     def all_to_all_async(self, out, inp):
         """all_to_all on a side stream after the current stream's work; wait() orders the current stream after it."""

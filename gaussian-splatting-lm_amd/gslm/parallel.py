@@ -85,6 +85,10 @@ def shard_views(n_views, rank, world_size):
 
 def _all_gather_into(out, inp, group=None):
     """out[r * len(inp):(r + 1) * len(inp)] = rank r's inp (dim 0 blocks)."""
+    nc = native_comm(group, out.device) if out.is_cuda else None
+    if nc is not None:
+        nc.all_gather(out, inp)
+        return
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, inp, group=group)
         return

@@ -449,6 +449,9 @@ int gslm_allreduce_sum_f64(void* comm, double* buf, int64_t n, void* stream);
 /* recv[r * bytes_per_rank ...] = rank r's send[rank * bytes_per_rank ...] (the Gaussian-sharded exchange's records
  * and screen sums, gslm_tangent_views / GSLM_STAGE_SCREEN) */
 int gslm_alltoall(void* comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream);
+/* recv[r * bytes_per_rank ...] = rank r's send[0 .. bytes_per_rank) (the screen exchange's per-view sums,
+ * gslm_gather_screen) */
+int gslm_allgather(void* comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream);
 
 /* ---- LM residual epilogue of one view (replaces the render clamp
  * gaussian_renderer/batch_render.py:118 + compute_batch_loss_block, solver/batch_training_loss.py:10-17,

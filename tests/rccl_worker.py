@@ -68,6 +68,17 @@ def main():
             from gslm.parallel import _NATIVE
             out["native"] = {"comm_made": len(_NATIVE) > 0, "y_bitwise": bool(torch.equal(y, res[0][0])),
                              "x_bitwise": bool(torch.equal(x, x_t))}
+        if mode in ("screen", "allreduce"):
+            # the screen exchange's all-gather (gslm_allgather) and the param-space all-reduce (gslm_allreduce_sum_f32)
+            # through the C-ABI communicator: the same product, bitwise
+            v = got.get("v")
+            vv = (torch.randn(op.layout.numel, generator=torch.Generator().manual_seed(7)) if v is None else v).cuda()
+            y_t = op.matvec(vv, op.zeros())
+            os.environ["GSLM_COMM"] = "native"
+            y_n = op.matvec(vv, op.zeros())
+            torch.cuda.synchronize()
+            del os.environ["GSLM_COMM"]
+            out["exchanges"][mode]["native_bitwise"] = bool(torch.equal(y_t, y_n))
     # the C-ABI collectives on their own (one rank): sums and the all-to-all are identities / copies
     from gslm.comm import NativeComm
     nc = NativeComm(device="cuda")
@@ -80,8 +91,11 @@ def main():
     src = torch.arange(4096, dtype=torch.int32, device="cuda")
     dst = torch.zeros_like(src)
     nc.all_to_all_async(dst, src).wait()
+    gat = torch.zeros_like(src)
+    nc.all_gather(gat, src)
     torch.cuda.synchronize()
-    out["native"]["primitives"] = bool(torch.equal(a, a0) and torch.equal(d64, d0) and torch.equal(dst, src))
+    out["native"]["primitives"] = bool(torch.equal(a, a0) and torch.equal(d64, d0) and torch.equal(dst, src) and
+                                       torch.equal(gat, src))
     nc.close()
     # the whole LM step (train_jvp.py:237-279) on the sharded path: Gaussian-sharded CG + all-reduced line search
     import numpy as np

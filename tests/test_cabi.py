@@ -239,5 +239,6 @@ def test_comm_entry_points_check_arguments():
     assert lib.gslm_allreduce_sum_f32(None, None, 4, None) == -1
     assert lib.gslm_allreduce_sum_f64(None, None, 4, None) == -1
     assert lib.gslm_alltoall(None, None, None, 16, None) == -1
+    assert lib.gslm_allgather(None, None, None, 16, None) == -1
     assert b"NULL" in lib.gslm_last_error()
     assert lib.gslm_comm_destroy(None) == 0

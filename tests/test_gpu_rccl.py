@@ -37,6 +37,7 @@ def test_exchanges_through_rccl_one_rank():
     # CG iterates bitwise, and its collectives alone are identities at one rank
     nat = res["native"]
     assert nat["comm_made"] and nat["y_bitwise"] and nat["x_bitwise"] and nat["primitives"], nat
+    assert res["exchanges"]["screen"]["native_bitwise"] and res["exchanges"]["allreduce"]["native_bitwise"], res
     lm = res["lm_step"]  # the sharded LM step through RCCL against the reference's (lm_step_golden.npz)
     assert lm["ranks"] == 1 and lm["best_alpha"] == lm["best_alpha_ref"], lm
     assert lm["step_rel"] <= 1e-4 and lm["final_rel"] <= 1e-4, lm
