@@ -8,6 +8,15 @@ namespace gslm {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+thread_local DebugSync g_debug;
+
+int launch_failed(hipError_t e, const char* file, int line) {
+  const char* base = std::strrchr(file, '/');
+  set_error(std::string(g_debug.on ? "kernel failed (debug mode: stream synchronised after the launch at " : "kernel launch (") +
+            (base ? base + 1 : file) + ":" + std::to_string(line) + "): " + hipGetErrorString(e));
+  return GSLM_ERR_HIP;
+}
+
 namespace {
 
 struct Carver {
@@ -220,6 +229,7 @@ size_t gslm_scratch_bytes(int64_t P, int64_t N) { return scratch_layout(P, N, nu
 
 int gslm_preprocess(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, int32_t* out_radii,
                     void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   ViewK v;
   GaussK g;
   int st = make_view(view, gi ? gi->max_coeffs : 0, &v);
@@ -315,6 +325,7 @@ int gslm_num_rendered_many(const void* const* geoms, const int64_t* Ps, int32_t 
 int gslm_rasterize(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes,
                    int64_t N, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
                    void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
@@ -370,6 +381,7 @@ int64_t gslm_binning_capacity(size_t binning_bytes, int32_t H, int32_t W) {
 
 int gslm_rasterize_dev(const gslm_view* view, int64_t P, void* geom, void* binning, size_t binning_bytes, void* image,
                        size_t image_bytes, float* out_color, float* out_invdepth, uint32_t* n_out, void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
@@ -522,6 +534,7 @@ int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* str
 int gslm_forward(const gslm_view* view, const gslm_gaussians* gi, void* geom, size_t geom_bytes, void* binning,
                  size_t binning_bytes, void* image, size_t image_bytes, float* out_color, float* out_invdepth,
                  int32_t* out_radii, int64_t* out_num_rendered, void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   int st = gslm_preprocess(view, gi, geom, geom_bytes, out_radii, stream);
   if (st) return st;
   int64_t N = 0;
@@ -599,6 +612,7 @@ static int bind_all(const gslm_view* view, const gslm_gaussians* gi, const void*
 int gslm_backward(const gslm_view* view, const gslm_gaussians* gi, const void* geom, const void* binning, int64_t N,
                   const void* image, const float* dL_dcolor, const float* dL_dinvdepth, void* scratch,
                   size_t scratch_bytes, const gslm_grads* out, void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;
@@ -611,6 +625,7 @@ int gslm_backward(const gslm_view* view, const gslm_gaussians* gi, const void* g
 int gslm_jvp(const gslm_view* view, const gslm_gaussians* gi, const gslm_gaussians* tangent,
              const float* means2D_tangent, const void* geom, const void* binning, int64_t N, const void* image,
              void* scratch, size_t scratch_bytes, float* out_color_t, float* out_invdepth_t, void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;
@@ -671,6 +686,7 @@ int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* gi, const g
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,
                         int64_t N, const void* image, void* scratch, size_t scratch_bytes, const gslm_grads* y,
                         const gslm_matvec_opts* opts, void* stream) {
+  DebugScope dbg_scope(view != nullptr && view->debug != 0, stream);
   Bound b;
   int st = bind_all(view, gi, geom, binning, N, image, scratch, scratch_bytes, &b);
   if (st) return st;

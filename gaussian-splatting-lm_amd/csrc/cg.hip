@@ -104,7 +104,7 @@ __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const doub
                                                            const float* __restrict__ g, double* __restrict__ part,
                                                            const double* __restrict__ ctl) {
   __shared__ double sm[DOT_THREADS / 64];
-  if (ctl && (ctl[0] != 0.0 || *del < 1e-20)) return;
+  if (ctl && (ctl[0] != 0.0 || *del < 1e-20 || !isfinite(*del))) return;  // a NaN delta: x kept (stop 4 below)
   const float a = (float)((*gam) / (*del));
   double acc = 0.0, axg = 0.0, axs = 0.0;
   const int64_t n4 = n / 4;
@@ -167,12 +167,19 @@ __global__ __launch_bounds__(DOT_THREADS) void k_cg_update(int64_t n, const doub
 //   res > last_res                      -> stop = 2 (after the step, as the reference breaks after x += alpha p)
 //   gamma' < max(tol sqrt(gamma), atol) -> stop = 3
 //   otherwise iters += 1 (iter_total).  A stopped solve's later kernels return at once (ViewK::stop, k_cg_update).
+// Failure detection first (the NaN asserts of matvec_T, solver_functions.py:125-130): a non-finite gamma, gamma',
+// delta, <x, g> or <x, s> -- a NaN or Inf anywhere in J^T b, in a product (J^T J + D) p or in the iterate reaches
+// these dots -- sets stop = 4 (GSLM_CG_STOP_NONFINITE) and nothing else; the host raises before the step is used.
 // Same double arithmetic as the host-side tests of gslm.lm.cgls_fused.
 __global__ void k_cg_monitor(const double* __restrict__ gam, const double* __restrict__ gamn,
                              const double* __restrict__ del, const double* __restrict__ xg,
                              const double* __restrict__ xs, const double* __restrict__ b2, double tol, double atol,
                              double* __restrict__ ctl, int max_hist) {
   if (threadIdx.x != 0 || ctl[0] != 0.0) return;
+  if (!(isfinite(*gam) && isfinite(*gamn) && isfinite(*del) && isfinite(*xg) && isfinite(*xs))) {
+    ctl[0] = 4.0;
+    return;
+  }
   if (*del < 1e-20) {
     ctl[0] = 1.0;
     return;

@@ -147,9 +147,11 @@ __global__ __launch_bounds__(256) void k_preprocess_dma(ViewK v, GaussK g, float
 // 84 B of its outputs; the block loads its Gaussians' inputs and stages their SH rows once, then writes every view's
 // records, depth keys, tile counts and rects from them.  Per view the same functions in the same order as
 // k_preprocess_dma: bitwise the same geometry.
-template <bool RAW>
+// STAGE: the block's SH-rest rows are staged in LDS by LDS-DMA (views_pass_ok); otherwise (SH degree 0, colours or
+// cov3D given, an odd layout) every view reads its inputs from global memory -- the same outputs, depth space included.
+template <bool RAW, bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess_views(PreViewsK pv, GaussK g) {
-  extern __shared__ __attribute__((aligned(16))) float s_sh[];  // [256 * rest_stride]
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];  // [256 * rest_stride] (STAGE)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = i0 + tid;
@@ -158,27 +160,34 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PreViewsK pv, GaussK g
   if (live) load_pre_in<RAW>(g, i, in);
   asm volatile("" : : "v"(in.x), "v"(in.y), "v"(in.z), "v"(in.c[0]), "v"(in.c[1]), "v"(in.c[2]), "v"(in.c[3]),
                "v"(in.c[4]), "v"(in.c[5]), "v"(in.qw), "v"(in.op));
-  const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
-  const int64_t total = nv * g.rest_stride;
-  const int64_t n4 = total / 4;
-  const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
-  float4* dst4 = reinterpret_cast<float4*>(s_sh);
-  for (int64_t c = w; c * 64 < n4; c += 4) {
-    const int64_t e = min(c * 64 + lane, n4 - 1);
-    glds16(src4 + e, dst4 + c * 64);
+  int64_t total = 0, n4 = 0;
+  if constexpr (STAGE) {
+    const int64_t nv = min((int64_t)blockDim.x, g.P - i0);
+    total = nv * g.rest_stride;
+    n4 = total / 4;
+    const float4* src4 = reinterpret_cast<const float4*>(g.rest + i0 * g.rest_stride);
+    float4* dst4 = reinterpret_cast<float4*>(s_sh);
+    for (int64_t c = w; c * 64 < n4; c += 4) {
+      const int64_t e = min(c * 64 + lane, n4 - 1);
+      glds16(src4 + e, dst4 + c * 64);
+    }
   }
   // view 0's geometry while the rows land (as k_preprocess_dma)
   PreOut o0;
   o0.depth = 0.f;
   const bool vis0 = live && preprocess_core<RAW, false>(pv.v[0], g, i, in, o0);
-  __syncthreads();
-  if (n4 * 4 < total) {
-    for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+  if constexpr (STAGE) {
     __syncthreads();
+    if (n4 * 4 < total) {
+      for (int64_t e = n4 * 4 + tid; e < total; e += blockDim.x) s_sh[e] = g.rest[i0 * g.rest_stride + e];
+      __syncthreads();
+    }
   }
   if (!live) return;
-  g.rest = s_sh;
-  g.rest_base = i0;
+  if constexpr (STAGE) {
+    g.rest = s_sh;
+    g.rest_base = i0;
+  }
 #pragma unroll 1
   for (int b = 0; b < pv.n; ++b) {
     const ViewK& v = pv.v[b];
@@ -224,24 +233,26 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PreViewsK pv, GaussK g
   }
 }
 
-// whether k_preprocess_views applies: raw GaussianModel leaves with the SH rest as its contiguous 16-B aligned leaf
-// (otherwise launch_preprocess_views runs launch_preprocess per view)
+// whether k_preprocess_views can stage the SH rows: raw GaussianModel leaves with the SH rest as its contiguous 16-B
+// aligned leaf (otherwise the unstaged instantiation runs; until round 5 a per-view launch_preprocess did, which
+// ignored the depth positions of the line search's union workspaces: ADVICE r04)
 static bool views_pass_ok(const GaussK& g) {
   return g.raw && !g.colors && !g.cov3D && g.rest && g.M > 1 && g.rest_stride == 3 * (g.M - 1) &&
          ((uintptr_t)g.rest & 15u) == 0;
 }
 
 int launch_preprocess_views(const PreViewsK& pv, const GaussK& g, const GeomBufs* gbs, hipStream_t s) {
+  (void)gbs;
   if (g.P == 0 || pv.n == 0) return GSLM_OK;
-  if (!views_pass_ok(g)) {
-    for (int b = 0; b < pv.n; ++b) {
-      const int st = launch_preprocess(pv.v[b], g, gbs[b], nullptr, s);
-      if (st) return st;
-    }
-    return GSLM_OK;
+  const dim3 grid((unsigned)((g.P + 255) / 256));
+  if (views_pass_ok(g)) {
+    const size_t lds = (size_t)256 * g.rest_stride * sizeof(float);
+    hipLaunchKernelGGL((k_preprocess_views<true, true>), grid, dim3(256), lds, s, pv, g);
+  } else if (g.raw) {  // every layout and both output spaces (depth positions included): no per-view fallback
+    hipLaunchKernelGGL((k_preprocess_views<true, false>), grid, dim3(256), 0, s, pv, g);
+  } else {
+    hipLaunchKernelGGL((k_preprocess_views<false, false>), grid, dim3(256), 0, s, pv, g);
   }
-  const size_t lds = (size_t)256 * g.rest_stride * sizeof(float);
-  hipLaunchKernelGGL(k_preprocess_views<true>, dim3((unsigned)((g.P + 255) / 256)), dim3(256), lds, s, pv, g);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -312,14 +323,15 @@ __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint
 // costliest tiles do not start last and set the kernel's tail).  One block; buckets of the length
 // (exact below 768 entries, 32-wide above), order inside a bucket arbitrary.  Only scheduling
 // changes: every tile's results are independent of when it runs.
+// cost (or NULL): a per-tile cost key instead of the list length (k_tile_cost: the LM product's modelled wave-visits).
 __global__ __launch_bounds__(1024) void k_tile_order(int ntiles, const uint2* __restrict__ ranges,
-                                                      uint32_t* __restrict__ order) {
+                                                      uint32_t* __restrict__ order, const uint32_t* __restrict__ cost) {
   __shared__ uint32_t s_cnt[1024];
   const int tid = threadIdx.x;
   s_cnt[tid] = 0u;
   __syncthreads();
   auto bucket = [&](int t) {
-    const uint32_t n = ranges[t].y - ranges[t].x;
+    const uint32_t n = cost ? cost[t] : ranges[t].y - ranges[t].x;
     return 1023u - (n < 768u ? n : min(1023u, 768u + ((n - 768u) >> 5)));  // heaviest first
   };
   for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
@@ -376,6 +388,55 @@ __global__ __launch_bounds__(256) void k_tile_neff(ViewK v, const uint32_t* __re
   if ((threadIdx.x & 63) == 0) neff[4 * tile + (threadIdx.x >> 6)] = (uint32_t)wm;
 }
 
+// The LM product's cost of a tile, in wave-visits (k_render_matvec's schedule model): the J v pass runs one
+// independent wave per quadrant, so its busiest wave -- the largest count over quadrants q of the list positions
+// below the quadrant's bound neff[q] whose mask holds q -- sets its time; the VJP pass runs 128-entry batches from
+// max_q neff down with a block barrier around each, so every batch costs its busiest wave's count.  Cost = the two
+// summed.  Tiles ordered by it (k_tile_order) schedule the product's blocks longest-first by what they actually do:
+// the list length, the forward's key, ranks them by entries no LM pass visits (tools/exp/tile_sched.py: modelled
+// idle tail 11.8% of the launch by length, 5.3% by this cost).  One block per tile; threads 0..127 take batch b,
+// 128..255 batch b + 1 (two waves per batch).
+__global__ __launch_bounds__(256) void k_tile_cost(const uint2* __restrict__ ranges,
+                                                    const uint32_t* __restrict__ point_list,
+                                                    const uint32_t* __restrict__ neff, uint32_t* __restrict__ cost) {
+  __shared__ uint32_t s_c[4][4];  // [wave][quadrant] counts of the current pair of batches
+  const int tile = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  const uint2 r = ranges[tile];
+  const uint32_t len = r.y - r.x;
+  uint32_t wm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wm[q] = min(neff[4 * tile + q], len);
+  const int n_eff = (int)max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+  uint32_t tot[4] = {0u, 0u, 0u, 0u}, vjp = 0u;
+  for (int base = 0; base < n_eff; base += 256) {
+    // batch b = base / 128 + (tid >> 7): list position n_eff - 1 - (base + tid)
+    const int pos = n_eff - 1 - (base + tid);
+    uint32_t m = 0u;
+    if (pos >= 0) {
+      const uint32_t e = point_list[r.x + pos];
+      m = pl_mask(e) & (((uint32_t)pos < wm[0] ? 1u : 0u) | ((uint32_t)pos < wm[1] ? 2u : 0u) |
+                        ((uint32_t)pos < wm[2] ? 4u : 0u) | ((uint32_t)pos < wm[3] ? 8u : 0u));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t c = (uint32_t)__popcll(__ballot((m >> q) & 1u));
+      if ((tid & 63) == 0) s_c[w][q] = c;
+    }
+    __syncthreads();
+    uint32_t b0 = 0u, b1 = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t c0 = s_c[0][q] + s_c[1][q], c1 = s_c[2][q] + s_c[3][q];
+      tot[q] += c0 + c1;
+      b0 = max(b0, c0);
+      b1 = max(b1, c1);
+    }
+    vjp += b0 + b1;
+    __syncthreads();
+  }
+  if (tid == 0) cost[tile] = max(max(tot[0], tot[1]), max(tot[2], tot[3])) + vjp;
+}
+
 // The quadrants whose pixels still blend at list position pos (vjp_tile's per-wave bounds) and the entry's
 // effective mask: its quadrant mask restricted to them.  A head entry is one with a non-empty effective mask.
 __device__ __forceinline__ uint32_t eff_mask(uint32_t e, uint32_t pos, const uint32_t* wm4) {
@@ -415,6 +476,12 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
   }
   const unsigned nb = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_tile_neff, dim3(ntiles), dim3(TILE_PIX), 0, s, v, ib.n_contrib, bb.tile_neff);
+  if (N + 1 >= ntiles) {
+    // the LM tile passes' launch order by their modelled cost (hscan holds the costs until k_row_flags rewrites it;
+    // only the schedule changes, every tile's results are independent of when it runs)
+    hipLaunchKernelGGL(k_tile_cost, dim3(ntiles), dim3(256), 0, s, bb.ranges, bb.point_list, bb.tile_neff, sb.hscan);
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, sb.hscan);
+  }
   hipLaunchKernelGGL(k_row_flags, dim3(nb), dim3(256), 0, s, N, v.gx, bb.keys_sorted, bb.point_list, bb.ranges,
                      bb.tile_neff, gb.goff, gb.rect, bb.slots, sb.hscan);
   GSLM_LAUNCH_CHECK();
@@ -617,7 +684,7 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
                        (uint32_t*)nullptr);
     GSLM_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
+  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -677,7 +744,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
       if (P > 0) GSLM_HIP_CHECK(hipMemcpyAsync(n_out, gb.counters, 4, hipMemcpyDeviceToDevice, s));
       else GSLM_HIP_CHECK(hipMemsetAsync(n_out, 0, 4, s));
     }
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
     GSLM_LAUNCH_CHECK();
     return GSLM_OK;
   }
@@ -692,7 +759,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   const unsigned nbN = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, n_dev, n_out);
   GSLM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order);
+  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -51,6 +51,11 @@ struct ViewK {
   const double* stop = nullptr;
 };
 
+// torch.clamp(x, 0, 1) (the reference's rendered_image.clamp(0, 1), batch_render.py:118): a NaN stays a NaN, as in
+// torch -- fminf / fmaxf would turn it into 0 or 1 and hide it from the reference's NaN asserts (solver_functions.py:
+// 125-130).  Identical to fminf(fmaxf(x, 0), 1) for every other input.
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
 // block-uniform early exit of a product kernel once the device-side CG stopping tests fired
 __device__ __forceinline__ bool cg_stopped(const ViewK& v) { return v.stop != nullptr && *v.stop != 0.0; }
 

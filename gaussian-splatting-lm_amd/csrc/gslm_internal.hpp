@@ -20,13 +20,29 @@ void set_error(const std::string& msg);
     }                                                                                         \
   } while (0)
 
+// Debug mode (gslm_view.debug, the rasterizer settings' `debug`, arguments/__init__.py:70): upstream's CHECK_CUDA
+// synchronises after each kernel and throws on an error, so a failing launch is reported where it happened instead of
+// as a late status of some later call.  The drop-in entry points open a DebugScope for their stream; inside it every
+// GSLM_LAUNCH_CHECK synchronises that stream and names the launch site.
+struct DebugSync {
+  hipStream_t s = nullptr;
+  bool on = false;
+};
+extern thread_local DebugSync g_debug;
+struct DebugScope {
+  DebugSync prev;
+  DebugScope(bool on, void* stream) : prev(g_debug) {
+    if (on) g_debug = DebugSync{(hipStream_t)stream, true};
+  }
+  ~DebugScope() { g_debug = prev; }
+};
+int launch_failed(hipError_t e, const char* file, int line);  // sets the error (debug: with the launch site)
+
 #define GSLM_LAUNCH_CHECK()                                                                   \
   do {                                                                                        \
     hipError_t _e = hipGetLastError();                                                        \
-    if (_e != hipSuccess) {                                                                   \
-      ::gslm::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));              \
-      return GSLM_ERR_HIP;                                                                    \
-    }                                                                                         \
+    if (_e == hipSuccess && ::gslm::g_debug.on) _e = hipStreamSynchronize(::gslm::g_debug.s);  \
+    if (_e != hipSuccess) return ::gslm::launch_failed(_e, __FILE__, __LINE__);               \
   } while (0)
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }

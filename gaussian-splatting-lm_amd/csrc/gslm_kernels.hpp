@@ -321,7 +321,7 @@ __device__ __forceinline__ void preprocess_color(const ViewK& v, const GaussK& g
     for (int ch = 0; ch < 3; ++ch) {
       const float r = sh_color(v.D, dx, dy, dz, shf, ch);
       if (r < 0.0f) o.clamped |= (1u << ch);
-      o.rgb[ch] = fmaxf(r, 0.0f);
+      o.rgb[ch] = r < 0.0f ? 0.0f : r;  // upstream's glm::max(result, 0): a NaN coefficient stays a NaN colour
     }
   }
 }

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       const float R[3] = {C0 + T * v.bg[0], C1 + T * v.bg[1], C2 + T * v.bg[2]};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float r = m * fminf(fmaxf(R[c], 0.0f), 1.0f) - gt[c * HW + pid];
+        const float r = m * clamp01(R[c]) - gt[c * HW + pid];
         acc += (double)r * (double)r;
       }
     }
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
       const float R[3] = {C0[a] + Tf * v.bg[0], C1[a] + Tf * v.bg[1], C2[a] + Tf * v.bg[2]};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float r = mv * fminf(fmaxf(R[c], 0.0f), 1.0f) - gtc[c];
+        const float r = mv * clamp01(R[c]) - gtc[c];
         acc += (double)r * (double)r;
       }
     }

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_lm_residual(int64_t HW, const f
       const int64_t k = c * HW + p;
       const float R = color[k];
       const float inside = (R >= 0.0f && R <= 1.0f) ? 1.0f : 0.0f;
-      const float r = m * fminf(fmaxf(R, 0.0f), 1.0f) - gt[k];
+      const float r = m * clamp01(R) - gt[k];
       if (residual) residual[k] = r;
       if (weight) weight[k] = (m * m) * inside;
       if (seed) seed[k] = ((-2.0f * m) * inside) * r;

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_ssim_eval(SsimWin w, int H, int W, floa
   auto xval = [&](int c, int yy, int xx) {
     const int64_t p = (int64_t)yy * W + xx;
     const float m = mask ? mask[p] : 1.0f;
-    return m * fminf(fmaxf(color[c * HW + p], 0.0f), 1.0f);
+    return m * clamp01(color[c * HW + p]);
   };
   auto src = [&](int c, int yy, int xx, float v[5]) {
     const float x = xval(c, yy, xx), y = gt[c * HW + (int64_t)yy * W + xx];
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_ssim_eval(SsimWin w, int H, int W, floa
     const int64_t p = (int64_t)yy * W + xx;
     const float m = mask ? mask[p] : 1.0f;
     const float R = color[k];
-    const float x = m * fminf(fmaxf(R, 0.0f), 1.0f), y = gt[k];
+    const float x = m * clamp01(R), y = gt[k];
     const float mu1 = v[0], mu2 = v[1];
     const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
     const float s1 = v[2] - mu1_sq, s2 = v[3] - mu2_sq, s12 = v[4] - mu1_mu2;

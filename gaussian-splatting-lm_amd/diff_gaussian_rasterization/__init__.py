@@ -90,6 +90,29 @@ def forward_buffers(view, g, device):
     return color, radii, invdepth, geom, binning, image, N
 
 
+def _cpu_copy(args):
+    return tuple(a.detach().cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
+
+
+def _debug_call(settings, args, fn, which):
+    """Upstream's debug protocol (diff_gaussian_rasterization/__init__.py of the CUDA rasterizer, the `debug` of
+    arguments/__init__.py:70): copy the call's arguments to the host before the call, and on a failure save them to
+    snapshot_<which>.dump, say so, and re-raise.  The library side of debug mode (gslm_view.debug) synchronises after
+    every kernel so the failure is raised by the call that caused it."""
+    if not settings.debug:
+        return fn()
+    cpu_args = _cpu_copy(args)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    except Exception:
+        torch.save(cpu_args, f"snapshot_{which}.dump")
+        print(f"\nAn error occured in {'forward' if which == 'fw' else 'backward'}. "
+              f"Please forward snapshot_{which}.dump for debugging.")
+        raise
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(means3D, means2D, sh, dc, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -102,7 +125,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         s, r, c3 = _f32(scales), _f32(rotations), _f32(cov3Ds_precomp)
         shc, dcc, col = _f32(sh), _f32(dc), _f32(colors_precomp)
         g = _gaussians(P, m, o, s, r, c3, shc, dcc, col)
-        color, radii, invdepth, geom, binning, image, N = forward_buffers(view, g, device)
+        color, radii, invdepth, geom, binning, image, N = _debug_call(
+            raster_settings, (raster_settings.bg, means3D, colors_precomp, opacities, scales, rotations,
+                              raster_settings.scale_modifier, cov3Ds_precomp, raster_settings.viewmatrix,
+                              raster_settings.projmatrix, raster_settings.tanfovx, raster_settings.tanfovy,
+                              raster_settings.image_height, raster_settings.image_width, sh, dc,
+                              raster_settings.sh_degree, raster_settings.campos, raster_settings.prefiltered),
+            lambda: forward_buffers(view, g, device), "fw")
         nr = torch.tensor([N], dtype=torch.int64)
         return color, radii, invdepth, geom, binning, image, nr
 
@@ -147,10 +176,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         scratch = _lib.u8(lib.gslm_scratch_bytes(P, N), device)
         gc = grad_color.contiguous() if grad_color is not None else torch.zeros(3, st.image_height, st.image_width, device=device)
         gi = grad_invdepth.contiguous() if grad_invdepth is not None else None
-        check(lib.gslm_backward(ctypes.byref(view), ctypes.byref(g), geom.data_ptr(), binning.data_ptr(), N,
-                                image.data_ptr(), gc.data_ptr(), None if gi is None else gi.data_ptr(),
-                                scratch.data_ptr(), scratch.numel(), ctypes.byref(grads),
-                                _lib.stream_handle(device)), "gslm_backward")
+        _debug_call(st, (st.bg, means3D, opacities, scales, rotations, cov3Ds_precomp, sh, dc, colors_precomp, gc, gi,
+                         geom, binning, image, N),
+                    lambda: check(lib.gslm_backward(ctypes.byref(view), ctypes.byref(g), geom.data_ptr(),
+                                                    binning.data_ptr(), N, image.data_ptr(), gc.data_ptr(),
+                                                    None if gi is None else gi.data_ptr(), scratch.data_ptr(),
+                                                    scratch.numel(), ctypes.byref(grads), _lib.stream_handle(device)),
+                                  "gslm_backward"), "bw")
         sh_grad = d_sh if sh is not None and sh.numel() else None
         return (d_means3D, d_means2D, sh_grad, d_dc, d_col, d_opac, d_scales, d_rot, d_cov, None)
 

@@ -548,6 +548,31 @@ class LMProblem:
         return torch.zeros(self.layout.numel, dtype=torch.float32, device=self.device)
 
 
+class NonFiniteError(AssertionError):
+    """A NaN or Inf reached the normal equations.  The reference's only failure detection on the LM path is
+    matvec_T's `assert not torch.isnan(self.gaussians._<group>.grad).any(), "NaN detected in gaussians._<group>.grad"`
+    (solver/solver_functions.py:125-130), which aborts the step before the parameters move; this is raised at the
+    same point of the fused solve (an AssertionError, with the reference's message), before update_params."""
+
+
+CG_STOP_NONFINITE = 4  # gslm_cg_monitor's stop code (include/gslm.h GSLM_CG_STOP_NONFINITE)
+
+
+def raise_nonfinite(prob, g, what="the normal-equations product (J^T J + D) p"):
+    """Raises NonFiniteError naming the parameter groups of J^T b (= g) that hold a NaN / Inf, as the reference's
+    asserts do; when J^T b is finite the failure came later in the solve (a product or the iterate)."""
+    names = []
+    try:
+        for k, v in prob.layout.views(g).items():
+            if k != "exposure" and v.numel() and not bool(torch.isfinite(v).all()):
+                names.append(k)
+    except (AttributeError, RuntimeError, TypeError):
+        pass
+    if names:
+        raise NonFiniteError("; ".join(f"NaN detected in gaussians._{k}.grad" for k in names))
+    raise NonFiniteError(f"NaN detected in {what} during CGLS (J^T b is finite)")
+
+
 def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check_every=True, verbose=False,
                callback=None, host_checks=None):
     """cgls_damped (conjugate_gradient.py:51-127) on the fused operator, x0 = 0.
@@ -635,6 +660,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez, **ctl_kw):
                 prob.dot(p[lo:], q[lo:], ptr(DEL))
             reduce(DEL)
+            if check_every and not on_device and not math.isfinite(sc[DEL].item()):
+                raise_nonfinite(prob, g)
             if check_every and not on_device and sc[DEL].item() < 1e-20:
                 if verbose:
                     print("Early termination: delta is too small.")
@@ -662,6 +689,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
             pre = (s, ptr(GAMN), ptr(GAM))
             if check_every and not on_device:
                 vals = sc[:5].tolist()
+                if not all(math.isfinite(vals[k]) for k in (GAM, GAMN, XG, XS)):
+                    raise_nonfinite(prob, g)
                 res = b2 - vals[XG] - vals[XS]  # ||b - J x||^2 + x^T D x  (monitor of conjugate_gradient.py:103-104)
                 history.append(res)
                 if verbose:
@@ -685,6 +714,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     flush()
     if on_device:
         c = ctl.tolist()  # the solve's one read-back
+        if int(c[0]) == CG_STOP_NONFINITE:  # (the monitor's inputs are all-reduced first: every rank raises here)
+            raise_nonfinite(prob, g)
         iter_total, nh = int(c[1]), int(c[3])
         history = c[4:4 + min(nh, max_iter)]
         return x, {"iters": iter_total, "residuals": history, "stop": int(c[0])}
@@ -1189,6 +1220,11 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
         raise ValueError(f"recursion must be 'fused' or 'cgls', got {recursion!r}")
     # the whole step in the reference's layout, identical on every rank
     s = prob.gather_full(s) if getattr(prob, "exchange", None) == "gaussian" else getattr(prob, "expand", lambda v: v)(s)
+    if not bool(torch.isfinite(s).all()):
+        # the reference's NaN asserts (solver_functions.py:125-130) on the step itself, before update_params touches the
+        # model -- for solves without the device stopping tests (which raise inside cgls_fused, naming the groups);
+        # s is the gathered step, the same on every rank, so every rank raises here and none waits in a collective
+        raise NonFiniteError("NaN detected in the LM step (the CGLS solution)")
     start_loss = float(start_loss)
     del prob
     lap("cg_ms")

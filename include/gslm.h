@@ -55,8 +55,12 @@ typedef struct gslm_view {
   int32_t sh_degree;    /* active SH degree D */
   int32_t prefiltered;
   int32_t antialiasing;
-  int32_t debug;        /* nonzero: exhaustive tile traversal -- every wave visits every list entry, as
-                           upstream does (the quadrant cull is off; results are bit-identical either way) */
+  int32_t debug;        /* nonzero (the settings' `debug`, arguments/__init__.py:70): upstream's debug mode --
+                           gslm_preprocess / _rasterize(_dev) / _forward / _backward / _jvp / _matvec_view_ex
+                           synchronise their stream after every kernel and fail at the launch that faulted
+                           (gslm_last_error names its source line) -- and the exhaustive tile traversal: every
+                           wave visits every list entry, as upstream does (the quadrant cull is off; results are
+                           bit-identical either way) */
 } gslm_view;
 
 /* Per-Gaussian inputs.  With raw = 0 they are the activated tensors the rasterizer receives
@@ -410,8 +414,8 @@ int gslm_cg_update(int64_t n, const double* gam_dev, const double* del_dev, cons
                    float* x, float* s, void* scratch, double* gam_new_dev, void* stream);
 /* gslm_cg_update plus the residual monitor of conjugate_gradient.py:103-104 in the same pass:
  * *xg_dev = <x_new, g>, *xs_dev = <x_new, s_new> (g = J^T b).  scratch >= 3 * 1024 doubles.
- * cg_ctl (or NULL): gslm_cg_monitor's control block; with cg_ctl[0] != 0 or *del_dev < 1e-20 (the early
- * termination of conjugate_gradient.py:88-91) x and s are left untouched. */
+ * cg_ctl (or NULL): gslm_cg_monitor's control block; with cg_ctl[0] != 0, *del_dev < 1e-20 (the early
+ * termination of conjugate_gradient.py:88-91) or a non-finite *del_dev, x and s are left untouched. */
 int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_dev, const float* p, const float* q,
                            float* x, float* s, const float* g, void* scratch, size_t scratch_bytes,
                            double* gam_new_dev, double* xg_dev, double* xs_dev, const double* cg_ctl, void* stream);
@@ -420,7 +424,10 @@ int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_d
  * [stop, iters, last_res, n_hist, history[max_hist]], initialised by the caller to [0, 0, +inf, 0, ...]:
  *   *del < 1e-20 -> stop = 1;  res = (*b2 - *xg) - *xs is appended to history;  res > last_res -> stop = 2;
  *   *gam_new < max(tol sqrt(*gam), atol) -> stop = 3;  otherwise iters += 1.
+ * Checked before those: any of *gam, *gam_new, *del, *xg, *xs not finite -> stop = 4 (GSLM_CG_STOP_NONFINITE; the
+ * reference's NaN asserts, solver/solver_functions.py:125-130) -- the caller must not use the iterate.
  * Once stop != 0 every later gslm_cg_monitor / gslm_cg_update_monitor / product with opts->cg_ctl is a no-op. */
+#define GSLM_CG_STOP_NONFINITE 4
 int gslm_cg_monitor(const double* gam_dev, const double* gam_new_dev, const double* del_dev, const double* xg_dev,
                     const double* xs_dev, const double* b2_dev, double tol, double atol, double* cg_ctl,
                     int32_t max_hist, void* stream);

@@ -176,3 +176,38 @@ def test_sharded_lm_step_matches_reference_golden(tmp_path, tag, sched):
     for k, t in zip(GROUPS, r0["params"]):
         err = np.abs(t.numpy().astype(np.float64) - L[f"{tag}_out_{k}"]).max()
         assert err <= 1e-4 * scale + 1e-6, (k, err, scale)
+
+
+def _nan_worker(rank, world, port, out_path):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "gaussian-splatting-lm_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from gslm.lm import NonFiniteError, lm_step
+    from oracle.lm_ref import OracleLMProblem, OracleLossEvaluator, cgls_solver
+    L, m, cams, val = _golden_scene()
+    with torch.no_grad():
+        m._features_rest[7, 1, 2] = float("nan")  # one SH coefficient of one Gaussian, on every rank's replica
+    before = [t.detach().clone() for t in m.params()]
+    err = None
+    try:
+        lm_step(m, cams, val, torch.zeros(3), max_iter=2, restart_iter=1, device="cpu",
+                backend=(OracleLMProblem, OracleLossEvaluator, cgls_solver))
+    except NonFiniteError as e:
+        err = str(e)
+    same = all(torch.equal(a.view(torch.int32), b.detach().view(torch.int32)) for a, b in zip(before, m.params()))
+    torch.save({"err": err, "unchanged": same}, out_path + f".{rank}")
+    dist.barrier()  # both ranks reach here: neither is left waiting in a collective of the step
+    dist.destroy_process_group()
+
+
+def test_sharded_lm_step_nan_raises_on_every_rank(tmp_path):
+    """The reference's failure detection (solver/solver_functions.py:125-130 asserts no NaN in any gradient group)
+    across 2 ranks: a NaN in one SH coefficient makes lm_step raise NonFiniteError (an AssertionError) on BOTH ranks,
+    before update_params, so every replica of theta is bitwise unchanged and no rank hangs in a collective."""
+    out = str(tmp_path / "n")
+    mp.start_processes(_nan_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn", join=True)
+    for r in (0, 1):
+        got = torch.load(out + f".{r}", weights_only=True)
+        assert got["err"] is not None and "NaN detected" in got["err"], got
+        assert got["unchanged"]

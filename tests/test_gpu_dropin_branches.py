@@ -165,3 +165,33 @@ def test_dc_split_jvp_with_partial_tangents():
         rc = run("cpu", _oracle_call, ost)
         gc = run(DEV, _gpu_call, gst)
         assert _rel(gc, rc) < 1e-4, f"{which}: colour tangent rel err {_rel(gc, rc):.3e}"
+
+
+def test_debug_mode_same_results_and_snapshot_on_failure(tmp_path, monkeypatch):
+    """settings.debug (arguments/__init__.py:70, forwarded by render()): upstream's debug mode.  The library then
+    synchronises after every kernel of the call (gslm_view.debug, a failing launch reported at its source line) and
+    walks every list entry in every wave; the Python side copies the arguments to the host first and, on a failure,
+    saves them to snapshot_fw.dump / snapshot_bw.dump and re-raises.  Results are bitwise those of the normal mode."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    model, cams = make_scene("dense_2k_sh3_64x48")
+    cam = cams[0]
+    D = model.max_sh_degree
+    monkeypatch.chdir(tmp_path)
+    outs = []
+    for debug in (False, True):
+        st = gpu_settings(cam, D)._replace(debug=debug)
+        inp = {k: v.to(DEV).detach().requires_grad_(True) for k, v in _inputs(model, "scale_modifier_0.8").items()}
+        m2 = torch.zeros_like(inp["means3D"], requires_grad=True)
+        color, radii, invd = GaussianRasterizer(st)(means2D=m2, **inp)
+        (color.square().sum() + invd.sum()).backward()
+        outs.append([color.detach(), radii, invd.detach(), m2.grad] + [inp[k].grad for k in sorted(inp)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not (tmp_path / "snapshot_fw.dump").exists()
+    # an invalid call (SH degree out of range): raised by the call, arguments dumped as upstream does
+    bad = gpu_settings(cam, D)._replace(debug=True, sh_degree=7)
+    inp = {k: v.to(DEV) for k, v in _inputs(model, "scale_modifier_0.8").items()}
+    with pytest.raises(RuntimeError):
+        GaussianRasterizer(bad)(means2D=torch.zeros_like(inp["means3D"]), **inp)
+    snap = torch.load(tmp_path / "snapshot_fw.dump", weights_only=True)
+    assert torch.equal(snap[1], inp["means3D"].cpu())

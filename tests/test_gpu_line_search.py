@@ -86,6 +86,21 @@ def test_evaluate_points_equal_exact_renders(batch, streams):
     assert [float(x) for x in ev_u.evaluate_points(sets2)] == exact2
 
 
+@pytest.mark.parametrize("D", [0, 1])
+def test_evaluate_points_equal_exact_renders_low_sh_degree(D):
+    """SH degree 0 (no SH-rest leaf: the preprocess cannot stage SH rows and runs its unstaged form, which must still
+    write the records at their depth positions -- ADVICE r04) and degree 1."""
+    from gslm.lm import LossEvaluator
+    m, cams = _scene(D=D)
+    lay, s = _step(m)
+    ev_x = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
+    ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
+    sets, exact, _, _ = _points(m, lay, s, ev_x)
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+    ev_u.loss_sets = False
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+
+
 def test_evaluate_points_with_alpha_masks_and_culled_sets():
     """Alpha masks on the residual, and points where some Gaussians are culled (opacity driven below 1/255, so their
     quadrant masks are empty, and scales driven to zero-area rects) while other points keep them."""

@@ -172,3 +172,40 @@ def test_loss_evaluator_equals_lmproblem_evaluate():
     with torch.no_grad():
         m._xyz.add_(0.05 * torch.randn(m._xyz.shape, generator=torch.Generator().manual_seed(7)).cuda())
     assert close(ev.evaluate(), LMProblem(m, cams, torch.zeros(3)).evaluate())
+
+
+@pytest.mark.parametrize("check_every", [True, False])
+def test_lm_step_nan_raises_before_update(check_every):
+    """The reference's NaN asserts (solver/solver_functions.py:125-130): a NaN in one SH coefficient must make lm_step
+    raise -- from the device stopping tests (gslm_cg_monitor stop 4, naming the group as the reference does) or, with
+    the tests off, from the check of the step -- before update_params, leaving every parameter bitwise unchanged."""
+    from gslm.lm import NonFiniteError, lm_step
+    d, L, m, cams, val = _setup()
+    with torch.no_grad():
+        m._features_rest[11, 2, 0] = float("nan")
+    before = [t.detach().clone() for t in m.params()]
+    with pytest.raises(NonFiniteError) as ei:
+        lm_step(m, cams, val, torch.zeros(3), max_iter=2, restart_iter=1, check_every=check_every)
+    assert "NaN detected" in str(ei.value)
+    if check_every:
+        assert "gaussians._features_rest.grad" in str(ei.value) or "features_dc" in str(ei.value), str(ei.value)
+    for a, b in zip(before, m.params()):
+        assert torch.equal(a.view(torch.int32), b.detach().view(torch.int32))
+
+
+def test_cg_monitor_nonfinite_stop_code():
+    """gslm_cg_monitor: a non-finite delta / gamma / monitor dot sets stop = 4 (GSLM_CG_STOP_NONFINITE) and nothing
+    else; finite scalars keep the reference's tests."""
+    import ctypes
+    import math
+    from gslm import _lib
+    lib = _lib.lib
+    for bad in (2, 1, 0, 3, 4):
+        sc = torch.tensor([1.0, 0.5, 2.0, 0.1, 0.1, 10.0], dtype=torch.float64, device="cuda")  # gam gamn del xg xs b2
+        sc[bad] = math.nan if bad != 3 else math.inf
+        ctl = torch.tensor([0.0, 0.0, math.inf, 0.0, 0.0, 0.0], dtype=torch.float64, device="cuda")
+        p = lambda i: sc.data_ptr() + 8 * i
+        _lib.check(lib.gslm_cg_monitor(p(0), p(1), p(2), p(3), p(4), p(5), 1e-10, 0.0, ctl.data_ptr(), 2,
+                                       _lib.stream_handle()))
+        torch.cuda.synchronize()
+        assert ctl[0].item() == 4.0 and ctl[1].item() == 0.0 and ctl[3].item() == 0.0, (bad, ctl.tolist())
