@@ -177,21 +177,24 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
 }
 
 // the line search's shared binning: the n parameter sets' geometries, and the union list's per-set masks
-int union_sets(const void* const* geoms, int32_t n, int64_t P, UnionSets* u) {
+// the depth-space render records of gslm_preprocess_views(depth_pos): [P][RECS] float4 at the start of a workspace
+size_t depth_records_bytes(int64_t P) { return align_up((size_t)(P > 0 ? P : 0) * RECS * sizeof(float4)); }
+
+// the n per-set depth-space workspaces (each set_bytes long): only their render records are read
+int union_sets(const void* const* geoms, int32_t n, int64_t P, size_t set_bytes, UnionSets* u) {
   if (n < 1 || n > MAX_UNION_SETS) {
     set_error("union: 1 <= n <= 8 parameter sets");
     return GSLM_ERR_INVALID;
   }
   if (!geoms) { set_error("union: NULL geoms"); return GSLM_ERR_INVALID; }
+  if (set_bytes < depth_records_bytes(P)) { set_error("union: a set's workspace is below gslm_depth_records_bytes(P)"); return GSLM_ERR_CAPACITY; }
   *u = UnionSets{};
   u->n = n;
   for (int a = 0; a < n; ++a) {
     if (!geoms[a] && P) { set_error("union: NULL geometry"); return GSLM_ERR_INVALID; }
-    GeomBufs gb;
-    geom_layout(P, const_cast<void*>(geoms[a]), &gb);
-    u->rec[a] = gb.rec;
-    u->tiles[a] = gb.tiles;
-    u->rect[a] = gb.rect;
+    u->rec[a] = reinterpret_cast<const float4*>(geoms[a]);  // geom_layout's first region (rec at offset 0)
+    u->tiles[a] = nullptr;
+    u->rect[a] = nullptr;
   }
   return GSLM_OK;
 }
@@ -205,6 +208,7 @@ size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* o) {
   m.m0 = c.take<uint32_t>(N);
   m.m1 = c.take<uint32_t>(N);
   m.hist = c.take<uint32_t>(sort_hist_bytes(N, true) / 4);
+  m.nsets = c.take<uint32_t>(4);
   m.sorted = (bb.passes & 1) ? m.m1 : m.m0;
   if (o) *o = m;
   return c.off;
@@ -269,8 +273,9 @@ int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gau
   for (int b = 0; b < nviews; ++b) {
     if ((st = make_view(&views[b], gi->max_coeffs, &pv.v[b]))) return st;
     if ((st = make_gauss(gi, &pv.v[b], &g, false))) return st;  // each view's SH degree against the stored coefficients
-    if (geom_bytes < gslm_geom_bytes(g.P) || (!geoms[b] && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
-    geom_layout(g.P, geoms[b], &gbs[b]);
+    const size_t need = depth_pos ? depth_records_bytes(g.P) : gslm_geom_bytes(g.P);
+    if (geom_bytes < need || (!geoms[b] && g.P)) { set_error("geometry workspace too small"); return GSLM_ERR_CAPACITY; }
+    geom_layout(g.P, geoms[b], &gbs[b]);  // depth space writes the records (offset 0) only
     const uint32_t* pos = depth_pos ? depth_pos[b] : nullptr;
     if (depth_pos && !pos && g.P) { set_error("preprocess_views: NULL depth positions"); return GSLM_ERR_INVALID; }
     pv.out[b] = PreOutBufs{gbs[b].rec, gbs[b].depth_key, gbs[b].tiles, gbs[b].rect, gbs[b].clampw, pos};
@@ -425,15 +430,17 @@ size_t gslm_union_binning_bytes(int64_t N, int32_t H, int32_t W) {
   return union_masks_layout(N, ntiles, nullptr, nullptr);
 }
 
-int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, void* union_geom,
-                        size_t union_geom_bytes, void* stream) {
+size_t gslm_depth_records_bytes(int64_t P) { return depth_records_bytes(P); }
+
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
+                        void* union_geom, size_t union_geom_bytes, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
   if (P < 0 || P > MAX_P) { set_error("P out of range [0, 2^28 - 1]"); return GSLM_ERR_INVALID; }
   if (union_geom_bytes < gslm_geom_bytes(P) || (!union_geom && P)) { set_error("union geometry workspace too small"); return GSLM_ERR_CAPACITY; }
   UnionSets u;
-  if ((st = union_sets(geoms, n, P, &u))) return st;
+  if ((st = union_sets(geoms, n, P, set_bytes, &u))) return st;
   GeomBufs ug;
   geom_layout(P, union_geom, &ug);
   hipStream_t s = (hipStream_t)stream;
@@ -447,7 +454,7 @@ int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geo
 }
 
 int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,
-                       int64_t N, const void* const* geoms, int32_t n, void* stream) {
+                       int64_t N, const void* const* geoms, int32_t n, size_t set_bytes, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
@@ -455,23 +462,30 @@ int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom,
   if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
   if (P && !union_geom) { set_error("union_binning: NULL union geometry"); return GSLM_ERR_INVALID; }
   UnionSets u;
-  if ((st = union_sets(geoms, n, P, &u))) return st;
+  if ((st = union_sets(geoms, n, P, set_bytes, &u))) return st;
   GeomBufs ug;
   BinBufs bb;
   UnionMasks um;
   geom_layout(P, const_cast<void*>(union_geom), &ug);
   bin_layout(N, v.gx * v.gy, binning, &bb);
   union_masks_layout(N, v.gx * v.gy, binning, &um);
+  // the set count the masks are built for (gslm_rasterize_loss_slot renders a NaN loss for a slot past it)
+  GSLM_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(um.nsets), (int)n, 1, (hipStream_t)stream));
   return launch_union_binning(v, P, ug, bb, um, N, u, (hipStream_t)stream);
 }
 
-int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, const void* binning,
-                             size_t binning_bytes, int64_t N, int32_t slot, const float* gt, const float* alpha_mask,
-                             void* scratch, size_t scratch_bytes, double* loss_dev, int32_t accumulate, void* stream) {
+int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, size_t set_bytes, const void* binning,
+                             size_t binning_bytes, int64_t N, int32_t slot, int32_t n_sets, const float* gt,
+                             const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
+                             int32_t accumulate, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
-  if (slot < 0 || slot >= MAX_UNION_SETS) { set_error("rasterize_loss_slot: slot must be in [0, 8)"); return GSLM_ERR_INVALID; }
+  if (n_sets < 1 || n_sets > MAX_UNION_SETS || slot < 0 || slot >= n_sets) {
+    set_error("rasterize_loss_slot: need 0 <= slot < n_sets <= 8");
+    return GSLM_ERR_INVALID;
+  }
+  if (set_bytes < depth_records_bytes(P)) { set_error("rasterize_loss_slot: set workspace below gslm_depth_records_bytes(P)"); return GSLM_ERR_CAPACITY; }
   if (N < 0 || N > 0xFFFFFFFFll) { set_error("rasterize_loss_slot: N out of range"); return GSLM_ERR_INVALID; }
   if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
   if (scratch_bytes < gslm_loss_scratch_bytes(v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
@@ -484,16 +498,17 @@ int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom,
   bin_layout(N, v.gx * v.gy, const_cast<void*>(binning), &bb);
   union_masks_layout(N, v.gx * v.gy, const_cast<void*>(binning), &um);
   return launch_render_loss(v, gb, bb, gt, alpha_mask, (double*)scratch, loss_dev, accumulate ? 1 : 0,
-                            (hipStream_t)stream, N > 0 ? um.sorted : nullptr, 4 * slot);
+                            (hipStream_t)stream, N > 0 ? um.sorted : nullptr, 4 * slot, um.nsets);
 }
 
 size_t gslm_loss_sets_scratch_bytes(int32_t n, int32_t H, int32_t W) {
   return (size_t)(n > 0 ? n : 1) * gslm_loss_scratch_bytes(H, W);
 }
 
-int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, const void* binning,
-                             size_t binning_bytes, int64_t N, const float* gt, const float* alpha_mask, void* scratch,
-                             size_t scratch_bytes, double* const* loss_dev, int32_t accumulate, void* stream) {
+int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
+                             const void* binning, size_t binning_bytes, int64_t N, const float* gt,
+                             const float* alpha_mask, void* scratch, size_t scratch_bytes, double* const* loss_dev,
+                             int32_t accumulate, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
@@ -502,6 +517,7 @@ int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const
   if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
   if (scratch_bytes < gslm_loss_sets_scratch_bytes(n, v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
   if (!gt || !loss_dev || !scratch || !geoms) { set_error("rasterize_loss_sets: NULL gt / loss / scratch / geoms"); return GSLM_ERR_INVALID; }
+  if (set_bytes < depth_records_bytes(P)) { set_error("rasterize_loss_sets: set workspace below gslm_depth_records_bytes(P)"); return GSLM_ERR_CAPACITY; }
   SetRecsK sr{};
   LossPtrsK lp{};
   for (int a = 0; a < n; ++a) {

@@ -15,7 +15,7 @@ namespace gslm {
 // ROWF4 = 3: drop-in rows (screen position and inverse depth too); ROWF4 = 2: the LM rows of
 // k_render_matvec (xyz frozen, no depth term), which k_gather_lm consumes -- the J^T b of an LM step.
 template <bool WITH_XY, bool WITH_INV, int ROWF4>
-__global__ __launch_bounds__(256) void k_render_bwd(ViewK v, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(256, 8) void k_render_bwd(ViewK v, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ tile_order,
                                                      const uint32_t* __restrict__ point_list,
                                                      const float4* __restrict__ rec,

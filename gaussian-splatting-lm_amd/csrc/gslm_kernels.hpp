@@ -496,7 +496,7 @@ int launch_point_ids(const uint32_t* point_list, int64_t N, uint32_t* out, hipSt
 // k_duplicate_union) with the records of gb (that set's geometry) instead of the point list's own quadrant bits
 int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
                        double* part, double* loss, int accumulate, hipStream_t s, const uint32_t* amask = nullptr,
-                       int shift = 0);
+                       int shift = 0, const uint32_t* nsets = nullptr);
 // ---- the line search's shared binning (forward.hip, gslm_union_*) ----
 constexpr int MAX_UNION_SETS = 8;  // 4 mask bits per set in one uint32 per list entry
 struct UnionSets {
@@ -512,6 +512,7 @@ struct UnionMasks {
   uint32_t* m1;
   uint32_t* sorted;
   uint32_t* hist;  // the payload sort's histograms (sort_hist_bytes(N, true): more, smaller blocks than the pair sort)
+  uint32_t* nsets; // [4]: the set count gslm_union_binning built the masks for (a slot past it renders a NaN loss)
 };
 size_t union_masks_layout(int64_t N, int ntiles, void* binning, UnionMasks* out);
 // all sets' blends + losses over a union list in one pass (render_fwd.hip, gslm_rasterize_loss_sets)

@@ -308,8 +308,10 @@ int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const
 }
 
 // sum of the per-tile loss partials in tile order (deterministic), times 2 (the [r; r] aliasing)
+// nsets (or NULL): the union binning's recorded set count; slot >= *nsets (masks that were never built) -> NaN loss
 __global__ __launch_bounds__(256) void k_tile_loss_final(const double* __restrict__ part, int np, int accumulate,
-                                                          double* __restrict__ loss) {
+                                                          double* __restrict__ loss, const uint32_t* __restrict__ nsets,
+                                                          int slot) {
   __shared__ double s[4];
   double acc = 0.0;
   for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
@@ -318,7 +320,8 @@ __global__ __launch_bounds__(256) void k_tile_loss_final(const double* __restric
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    if (nsets && (uint32_t)slot >= *nsets) l = __longlong_as_double(0x7ff8000000000000ll);  // quiet NaN
     *loss = accumulate ? *loss + l : l;
   }
 }
@@ -340,7 +343,8 @@ int launch_render_fwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
 }
 
 int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, const float* gt, const float* mask,
-                       double* part, double* loss, int accumulate, hipStream_t s, const uint32_t* amask, int shift) {
+                       double* part, double* loss, int accumulate, hipStream_t s, const uint32_t* amask, int shift,
+                       const uint32_t* nsets) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) {
     if (!accumulate) GSLM_HIP_CHECK(hipMemsetAsync(loss, 0, sizeof(double), s));
@@ -354,7 +358,8 @@ int launch_render_loss(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, co
     hipLaunchKernelGGL((k_render_fwd_wave<FWD_LOSS, false>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges,
                        bb.tile_order, bb.point_list, gb.rec, (float*)nullptr, (float*)nullptr, (float*)nullptr,
                        (uint32_t*)nullptr, gt, mask, part, (const uint32_t*)nullptr, 0);
-  hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const double*)part, ntiles, accumulate, loss);
+  hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const double*)part, ntiles, accumulate, loss,
+                     amask ? nsets : nullptr, shift / 4);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

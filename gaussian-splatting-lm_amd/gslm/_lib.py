@@ -115,21 +115,24 @@ EXPORTS = {
                                                ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_num_rendered_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "gslm_union_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "gslm_depth_records_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gslm_union_geometry": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
-                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+                                           ctypes.c_int32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p]),
     "gslm_union_binning": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
-                                          ctypes.c_int32, ctypes.c_void_p]),
+                                          ctypes.c_int32, ctypes.c_size_t, ctypes.c_void_p]),
     "gslm_rasterize_loss_slot": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64, ctypes.c_void_p,
-                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int32,
-                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                                ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+                                                ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64,
+                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int32,
+                                                ctypes.c_void_p]),
     "gslm_loss_sets_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "gslm_rasterize_loss_sets": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64,
-                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p,
-                                                ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
-                                                ctypes.c_int32, ctypes.c_void_p]),
+                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_size_t,
+                                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p]),
     "gslm_forward": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.POINTER(GslmGaussians), ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -236,7 +239,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 8  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 9  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):
@@ -291,23 +294,39 @@ def stream_handle(device=None):
 # a stream synchronisation per read, and the drop-in Function reads the settings in its forward, backward and jvp.  A
 # camera's matrices are the same tensors call after call, so the copy is cached per tensor object, valid while the
 # tensor lives at the same version (any in-place write bumps it).
+# The key is the tensor object, its storage address and its version counter.  A write that bypasses the version counter
+# (through `t.data`, or an alias with a counter of its own) is not seen: set_host_cache(False) (or GSLM_HOST_CACHE=0)
+# turns the cache off for code that moves cameras that way (the reference never does: its Camera matrices are built
+# once, scene/cameras.py:80-89), and clear_host_cache() drops every entry.
 _HOST_CACHE = {}
+_HOST_CACHE_ON = [os.environ.get("GSLM_HOST_CACHE", "1") != "0"]
+
+
+def set_host_cache(enabled):
+    _HOST_CACHE_ON[0] = bool(enabled)
+    if not enabled:
+        _HOST_CACHE.clear()
+
+
+def clear_host_cache():
+    _HOST_CACHE.clear()
 
 
 def _host_floats(t, n):
     if isinstance(t, torch.Tensor):
-        hit = _HOST_CACHE.get(id(t))
-        if hit is not None and hit[0]() is t and hit[1] == t._version and hit[2] == n:
+        hit = _HOST_CACHE.get(id(t)) if _HOST_CACHE_ON[0] else None
+        if (hit is not None and hit[0]() is t and hit[1] == t._version and hit[2] == n and
+                hit[4] == t.data_ptr()):
             return hit[3]
         vals = [float(x) for x in t.detach().reshape(-1).to("cpu", torch.float32).tolist()][:n]
-        if t.is_cuda:
+        if t.is_cuda and _HOST_CACHE_ON[0]:
             import weakref
             key = id(t)
             try:
                 ref = weakref.ref(t, lambda _r, key=key: _HOST_CACHE.pop(key, None))
             except TypeError:
                 return vals
-            _HOST_CACHE[key] = (ref, t._version, n, vals)
+            _HOST_CACHE[key] = (ref, t._version, n, vals, t.data_ptr())
         return vals
     return [float(x) for x in list(t)][:n]
 

@@ -996,18 +996,39 @@ class LossEvaluator:
         return t
 
     def _uslot(self, par, k, n, P):
-        """Batch position k's geometries (n sets) and union geometry, of slot set `par` (two sets alternate over the
-        batches: a batch's preprocesses overwrite the slots of the batch before the previous one)."""
+        """Batch position k's depth-space records (n sets, gslm_depth_records_bytes(P) = 64 B per Gaussian each) and
+        union geometry (gslm_geom_bytes(P), ~112 B per Gaussian), of slot set `par` (two sets alternate over the
+        batches: a batch's preprocesses overwrite the slots of the batch before the previous one).  Peak device memory
+        of evaluate_points: 2 x batch x (64 n + 112) B per Gaussian (7.9 GB at 1M Gaussians, batch 8, n = 6; until
+        round 5 every set held a whole geometry workspace: 12.5 GB), plus the snapshots' five moving leaves per point
+        (param_snapshot) and one sort geometry; clear_val_cache() releases an evaluator lm_step kept."""
         sl = self.uslots[par][k]
-        nb = lib.gslm_geom_bytes(P)
+        nr, nb = lib.gslm_depth_records_bytes(P), lib.gslm_geom_bytes(P)
         while len(sl["geoms"]) < n:
             sl["geoms"].append(None)
         for a in range(n):
-            if sl["geoms"][a] is None or sl["geoms"][a].numel() < nb:
-                sl["geoms"][a] = _lib.u8(nb, self.device)
+            if sl["geoms"][a] is None or sl["geoms"][a].numel() < nr:
+                sl["geoms"][a] = _lib.u8(nr, self.device)
         if sl["ugeom"] is None or sl["ugeom"].numel() < nb:
             sl["ugeom"] = _lib.u8(nb, self.device)
         return sl
+
+    def _sort_geom(self, P):
+        """The full geometry workspace of the depth sorts of evaluate_points (main stream only)."""
+        t = getattr(self, "_sgeom", None)
+        if t is None or t.numel() < lib.gslm_geom_bytes(P):
+            t = self._sgeom = _lib.u8(lib.gslm_geom_bytes(P), self.device)
+        return t
+
+    def refresh_views(self, cams, bg, sh_degree):
+        """Rebuild the views from the cameras (their matrices now) and drop the cached depth order of every view whose
+        camera moved -- a kept evaluator (lm_step's _VAL_CACHE) then never renders with a stale pose."""
+        for i, c in enumerate(cams):
+            v = _lib.view_from_camera(c, bg, sh_degree)
+            if bytes(v) != bytes(self.views[i]):
+                self.views[i] = v
+                self._orders[i] = None
+                self._pos[i] = None
 
     def evaluate_points(self, sets):
         """The validation loss at each of n <= 8 parameter sets (snapshots sharing the model's frozen xyz: the six
@@ -1048,12 +1069,12 @@ class LossEvaluator:
             slots = [self._uslot(par, k, n, P) for k in range(len(idx))]
             # 1. each view's depth order (sorted once while xyz is unchanged) and its inverse, the depth positions
             for k, i in enumerate(idx):
-                if self._orders[i] is None:  # the sort of set 0's geometry (its records are rewritten below)
+                if self._orders[i] is None:  # the depth sort (set 0's geometry; only the order is kept)
                     self._orders[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
+                    sg = self._sort_geom(P)
                     check(lib.gslm_preprocess_ordered(ctypes.byref(self.views[i]), ctypes.byref(gs[0]),
-                                                      slots[k]["geoms"][0].data_ptr(), slots[k]["geoms"][0].numel(),
-                                                      None, self._orders[i].data_ptr(), 1, main_h),
-                          "gslm_preprocess_ordered")
+                                                      sg.data_ptr(), sg.numel(), None, self._orders[i].data_ptr(), 1,
+                                                      main_h), "gslm_preprocess_ordered")
                     self._pos[i] = None
                 if self._pos[i] is None:
                     self._pos[i] = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
@@ -1069,8 +1090,9 @@ class LossEvaluator:
             # 3. union geometries and their pair counts (main stream; the read-back waits for main only)
             for k, i in enumerate(idx):
                 ge = (ctypes.c_void_p * n)(*[slots[k]["geoms"][a].data_ptr() for a in range(n)])
-                check(lib.gslm_union_geometry(ctypes.byref(self.views[i]), P, ge, n, slots[k]["ugeom"].data_ptr(),
-                                              slots[k]["ugeom"].numel(), main_h), "gslm_union_geometry")
+                check(lib.gslm_union_geometry(ctypes.byref(self.views[i]), P, ge, n, slots[k]["geoms"][0].numel(),
+                                              slots[k]["ugeom"].data_ptr(), slots[k]["ugeom"].numel(), main_h),
+                      "gslm_union_geometry")
             ugeoms = (ctypes.c_void_p * len(idx))(*[sl["ugeom"].data_ptr() for sl in slots])
             Ps = (ctypes.c_int64 * len(idx))(*([P] * len(idx)))
             Ns = (ctypes.c_int64 * len(idx))()
@@ -1091,21 +1113,22 @@ class LossEvaluator:
                     bins[k] = _lib.u8(int(need * 1.25) + 4096, self.device)
                 binning = bins[k]
                 ge = (ctypes.c_void_p * n)(*[sl["geoms"][a].data_ptr() for a in range(n)])
+                sb = sl["geoms"][0].numel()
                 check(lib.gslm_union_binning(ctypes.byref(vw), P, sl["ugeom"].data_ptr(), binning.data_ptr(),
-                                             binning.numel(), N, ge, n, sh), "gslm_union_binning")
+                                             binning.numel(), N, ge, n, sb, sh), "gslm_union_binning")
                 m = self.masks[i]
                 if self.loss_sets:  # all sets in one pass over the union list
                     scr = self._sets_scratch(k, n, H, W)
                     lp = (ctypes.c_void_p * n)(*[losses[a].data_ptr() + 8 * i for a in range(n)])
-                    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, binning.data_ptr(), binning.numel(), N,
+                    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, sb, binning.data_ptr(), binning.numel(), N,
                                                        self.gts[i].data_ptr(), None if m is None else m.data_ptr(),
                                                        scr.data_ptr(), scr.numel() * 8, lp, 0, sh),
                           "gslm_rasterize_loss_sets")
                     continue
                 scr = self.loss_scratch[k % len(self.streams)]
                 for a in range(n):
-                    check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][a].data_ptr(), binning.data_ptr(),
-                                                       binning.numel(), N, a, self.gts[i].data_ptr(),
+                    check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][a].data_ptr(), sb,
+                                                       binning.data_ptr(), binning.numel(), N, a, n, self.gts[i].data_ptr(),
                                                        None if m is None else m.data_ptr(), scr.data_ptr(),
                                                        scr.numel() * 8, losses[a].data_ptr() + 8 * i, 0, sh),
                           "gslm_rasterize_loss_slot")
@@ -1160,9 +1183,15 @@ def update_params(model, layout, step, scale, skip_xyz=False):
 _VAL_CACHE = {}  # lm_step's last validation evaluator: {"last": (key, evaluator)}
 
 
+def clear_val_cache():
+    """Release the validation evaluator lm_step keeps between LM steps (its workspaces -- evaluate_points' peak, see
+    LossEvaluator._uslot -- the views' depth orders, and its references to the model and the validation cameras)."""
+    _VAL_CACHE.clear()
+
+
 def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, mask_xyz=True, check_every=True,
             verbose=False, device="cuda", sh_projection="auto", recursion="fused", exchange="auto", group=None,
-            val_batch=8, timing=False, backend=None, line_search="union", val_at_start=False):
+            val_batch=8, timing=False, backend=None, line_search="union", val_at_start=False, cache_val=True):
     """One LM step of train_jvp.py:237-289: loss, CGLS on the normal equations, backtracking line search.
 
     Single process: LMProblem over `cams` (with one training view the SH-rest group of the CG vectors is carried
@@ -1180,7 +1209,9 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     and their validation losses come from ONE binning per view, LossEvaluator.evaluate_points -- bitwise the losses of
     the sequential renders; the final point, known only after them, is rendered as before) or "exact" (train_jvp.py's
     order: update, render, update, ...).  val_at_start: also report the validation loss at the starting parameters
-    (one more evaluation, outside the reference's algorithm: it shows whether the step descends).
+    (one more evaluation, outside the reference's algorithm: it shows whether the step descends).  cache_val: keep the
+    validation evaluator for the next LM step (its workspaces and cached depth orders; clear_val_cache() releases it;
+    the views are rebuilt from the cameras every step, so a moved camera is rendered at its new pose).
     backend: (problem_cls, evaluator_cls, solver) replacing (LMProblem, LossEvaluator, cgls_fused) -- the CPU
     multi-process tests run this same driver, sharding and reductions on the oracle restatement."""
     import time
@@ -1236,15 +1267,18 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     vkey = (id(model), model.active_sh_degree, tuple(id(c) for c in mine_val), tuple(id(t) for p in imgs for t in p),
             str(device), val_batch, evaluator_cls, sharded, id(group),
             tuple(float(x) for x in torch.as_tensor(bg).reshape(-1).tolist()))
-    hit = _VAL_CACHE.get("last")
+    hit = _VAL_CACHE.get("last") if cache_val else None
     if hit is not None and hit[0] == vkey:
         val = hit[1]
+        if hasattr(val, "refresh_views"):
+            val.refresh_views(mine_val, bg, model.active_sh_degree)
     else:
         _VAL_CACHE.pop("last", None)
         val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
                             reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
-        val.held = (model, list(mine_val), imgs)
-        _VAL_CACHE["last"] = (vkey, val)
+        if cache_val:
+            val.held = (model, list(mine_val), imgs)
+            _VAL_CACHE["last"] = (vkey, val)
     val_start = float(val.evaluate()) if val_at_start else None
     if val_at_start:
         lap("val_start_ms")

@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 8
+#define GSLM_ABI_VERSION 9
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -128,7 +128,9 @@ int gslm_preprocess_ordered(const gslm_view* view, const gslm_gaussians* g, void
  * gslm_preprocess writes them, with no depth sort and no tile-count scan.  A Gaussian's 236 B of inputs (SH 3) are
  * read once for the views.  depth_pos (or NULL): per view the Gaussians' depth positions (gslm_depth_positions of the
  * view's depth order); then only the render records are written, each at its Gaussian's depth position, the rect
- * slot zero when culled -- the DEPTH SPACE the line search's union binning reads (below). */
+ * slot zero when culled -- the DEPTH SPACE the line search's union binning reads (below) -- and each geoms[b] needs
+ * only gslm_depth_records_bytes(P) (64 B per Gaussian; ABI 9).  Every layout and SH degree (ABI 9: degree 0 too). */
+size_t gslm_depth_records_bytes(int64_t P);
 int gslm_preprocess_views(const gslm_view* views, int32_t nviews, const gslm_gaussians* g, void* const* geoms,
                           size_t geom_bytes, const uint32_t* const* depth_pos, void* stream);
 /* depth_pos[depth_order[s]] = s for s < P (the inverse of a gslm_preprocess_ordered depth order). */
@@ -171,7 +173,10 @@ int gslm_rasterize_loss_dev(const gslm_view* view, int64_t P, void* geom, void* 
 /* Stream-ordered 4-byte copy of gslm_preprocess' pair count to dst (device or host-pinned); no synchronisation. */
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream);
 
-/* ---- The line search's shared binning (ABI 8) ----
+/* ---- The line search's shared binning (ABI 8; ABI 9: the per-set workspaces' size set_bytes, each
+ * >= gslm_depth_records_bytes(P), and n_sets for gslm_rasterize_loss_slot, checked against slot and against the set
+ * count gslm_union_binning recorded in the binning workspace -- a slot past it renders a NaN loss instead of a
+ * plausible background-only one) ----
  * train_jvp.py:262-277 renders every validation view at six points theta + alpha s (alpha = 2, 1, .., 1/16) of one step
  * s whose xyz group is masked (:221-227).  A view's Gaussians then keep their screen centre and depth order at every
  * point, and each point's exact point list is the subsequence of one list binned over the union of the points' rects:
@@ -189,22 +194,22 @@ int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* str
  *      slot a -- the same visits in the same order with the same records as the exact render: the same loss, bitwise.
  * The union list's values are depth positions (every pass reads the points' records coalesced in depth order). */
 size_t gslm_union_binning_bytes(int64_t num_rendered, int32_t H, int32_t W);
-int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, void* union_geom,
-                        size_t union_geom_bytes, void* stream);
+int gslm_union_geometry(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
+                        void* union_geom, size_t union_geom_bytes, void* stream);
 int gslm_union_binning(const gslm_view* view, int64_t P, const void* union_geom, void* binning, size_t binning_bytes,
-                       int64_t num_rendered, const void* const* geoms, int32_t n, void* stream);
-int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, const void* binning,
-                             size_t binning_bytes, int64_t num_rendered, int32_t slot, const float* gt,
+                       int64_t num_rendered, const void* const* geoms, int32_t n, size_t set_bytes, void* stream);
+int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom, size_t set_bytes, const void* binning,
+                             size_t binning_bytes, int64_t num_rendered, int32_t slot, int32_t n_sets, const float* gt,
                              const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
                              int32_t accumulate, void* stream);
 /* Step 4 for all n sets in one pass over the union list (the list walked once; set a + 1's records loaded while set
  * a's hits are visited): *loss_dev[a] = [*loss_dev[a] if accumulate] + set a's loss, bitwise each
  * gslm_rasterize_loss_slot(geoms[a], a).  scratch >= gslm_loss_sets_scratch_bytes(n, H, W). */
 size_t gslm_loss_sets_scratch_bytes(int32_t n, int32_t H, int32_t W);
-int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, const void* binning,
-                             size_t binning_bytes, int64_t num_rendered, const float* gt, const float* alpha_mask,
-                             void* scratch, size_t scratch_bytes, double* const* loss_dev, int32_t accumulate,
-                             void* stream);
+int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
+                             const void* binning, size_t binning_bytes, int64_t num_rendered, const float* gt,
+                             const float* alpha_mask, void* scratch, size_t scratch_bytes, double* const* loss_dev,
+                             int32_t accumulate, void* stream);
 /* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
  * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
  * gslm_rasterize with a larger buffer). */

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_sizes():
     from gslm import _lib
     lib = _lib.lib
-    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 9
     g1, g2 = lib.gslm_geom_bytes(1000), lib.gslm_geom_bytes(2000)
     assert 0 < g1 < g2
     assert lib.gslm_binning_bytes(10_000, 1080, 1920) > 10_000 * 16
@@ -92,19 +92,24 @@ def test_invalid_arguments_return_error_codes():
 
 
 def test_union_binning_argument_checks():
-    """The line search's shared binning (ABI 8): set counts outside 1..8, slots outside [0, 8), NULL workspaces and
-    short buffers are refused before any launch (host-side checks only: no GPU here)."""
+    """The line search's shared binning (ABI 8; ABI 9 adds each set workspace's size and n_sets): set counts outside
+    1..8, slots outside [0, n_sets), set workspaces below gslm_depth_records_bytes(P), NULL workspaces and short buffers
+    are refused before any launch (host-side checks only: no GPU here)."""
     from gslm import _lib
     lib = _lib.lib
     view = _lib.make_view(64, 64, 0.5, 0.5, [0, 0, 0], 1.0, [0.0] * 16, [0.0] * 16, 0, [0, 0, 0])
     vp = ctypes.byref(view)
     geoms = (ctypes.c_void_p * 9)(*([None] * 9))
     gb = lib.gslm_geom_bytes(10)
+    rb = lib.gslm_depth_records_bytes(10)
+    assert 10 * 64 <= rb < gb  # the depth-space sets hold their 64-B records only
     for n in (0, 9):
-        assert lib.gslm_union_geometry(vp, 10, geoms, n, 16, gb, None) == _lib.GSLM_ERR_INVALID
+        assert lib.gslm_union_geometry(vp, 10, geoms, n, rb, 16, gb, None) == _lib.GSLM_ERR_INVALID
         assert b"parameter sets" in lib.gslm_last_error()
-    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, gb - 1, None) == _lib.GSLM_ERR_CAPACITY
-    assert lib.gslm_union_geometry(vp, 10, geoms, 2, 16, gb, None) == _lib.GSLM_ERR_INVALID
+    assert lib.gslm_union_geometry(vp, 10, geoms, 2, rb, 16, gb - 1, None) == _lib.GSLM_ERR_CAPACITY
+    assert lib.gslm_union_geometry(vp, 10, geoms, 2, rb - 1, 16, gb, None) == _lib.GSLM_ERR_CAPACITY
+    assert b"gslm_depth_records_bytes" in lib.gslm_last_error()
+    assert lib.gslm_union_geometry(vp, 10, geoms, 2, rb, 16, gb, None) == _lib.GSLM_ERR_INVALID
     assert b"NULL geometry" in lib.gslm_last_error()
     assert lib.gslm_depth_positions(None, 10, None, None) == _lib.GSLM_ERR_INVALID
     views = (_lib.GslmView * 9)(*([view] * 9))
@@ -114,15 +119,18 @@ def test_union_binning_argument_checks():
     # the union list carries two more words per entry than a binning (the per-set masks' sort ping-pong)
     nb = lib.gslm_union_binning_bytes(100, 64, 64)
     assert nb >= lib.gslm_binning_bytes(100, 64, 64) + 2 * 100 * 4
-    assert lib.gslm_union_binning(vp, 10, 16, 16, nb - 1, 100, geoms, 2, None) == _lib.GSLM_ERR_CAPACITY
-    assert lib.gslm_union_binning(vp, 10, 16, 16, nb, 100, geoms, 0, None) == _lib.GSLM_ERR_INVALID
-    for slot in (-1, 8):
-        assert lib.gslm_rasterize_loss_slot(vp, 10, 16, 16, nb, 100, slot, 16, None, 16, 1 << 20, 16, 0,
-                                            None) == _lib.GSLM_ERR_INVALID
+    assert lib.gslm_union_binning(vp, 10, 16, 16, nb - 1, 100, geoms, 2, rb, None) == _lib.GSLM_ERR_CAPACITY
+    assert lib.gslm_union_binning(vp, 10, 16, 16, nb, 100, geoms, 0, rb, None) == _lib.GSLM_ERR_INVALID
+    assert lib.gslm_union_binning(vp, 10, 16, 16, nb, 100, geoms, 2, rb - 1, None) == _lib.GSLM_ERR_CAPACITY
+    for slot, n_sets in ((-1, 6), (8, 8), (6, 6), (2, 2), (0, 0), (0, 9)):
+        assert lib.gslm_rasterize_loss_slot(vp, 10, 16, rb, 16, nb, 100, slot, n_sets, 16, None, 16, 1 << 20, 16, 0,
+                                            None) == _lib.GSLM_ERR_INVALID, (slot, n_sets)
         assert b"slot" in lib.gslm_last_error()
-    assert lib.gslm_rasterize_loss_slot(vp, 10, 16, 16, nb - 1, 100, 0, 16, None, 16, 1 << 20, 16, 0,
+    assert lib.gslm_rasterize_loss_slot(vp, 10, 16, rb - 1, 16, nb, 100, 0, 6, 16, None, 16, 1 << 20, 16, 0,
                                         None) == _lib.GSLM_ERR_CAPACITY
-    assert lib.gslm_rasterize_loss_slot(vp, 10, 16, 16, nb, 100, 0, None, None, 16, 1 << 20, 16, 0,
+    assert lib.gslm_rasterize_loss_slot(vp, 10, 16, rb, 16, nb - 1, 100, 0, 6, 16, None, 16, 1 << 20, 16, 0,
+                                        None) == _lib.GSLM_ERR_CAPACITY
+    assert lib.gslm_rasterize_loss_slot(vp, 10, 16, rb, 16, nb, 100, 0, 6, None, None, 16, 1 << 20, 16, 0,
                                         None) == _lib.GSLM_ERR_INVALID
 
 

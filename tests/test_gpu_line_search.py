@@ -262,3 +262,30 @@ def test_evaluate_points_tiny_and_ragged(P):
     ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
     sets, exact, _, _ = _points(m, lay, s, ev_x)
     assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+
+
+def test_loss_slot_past_the_recorded_set_count_is_nan():
+    """ADVICE r04 (ABI 9): gslm_union_binning records the set count its masks were built for; a slot at or past it
+    (a caller passing a larger n_sets than the binning's) renders a NaN loss, not a plausible background-only one."""
+    import ctypes
+    import math
+    from gslm import _lib
+    from gslm.lm import LossEvaluator, param_snapshot
+    lib = _lib.lib
+    m, cams = _scene(nviews=1)
+    ev = LossEvaluator(m, cams, torch.zeros(3), batch=1, streams=1)
+    sets = [param_snapshot(m), param_snapshot(m)]
+    got = [float(x) for x in ev.evaluate_points(sets)]
+    assert got[0] == got[1] == float(ev.evaluate())
+    # the evaluator's last union binning (batch position 0, view 0) was built for n = 2
+    sl, binning, vw = ev.uslots[0][0], ev.ubins[0], ev.views[0]
+    P, N = m._xyz.shape[0], ev.union_counts[0]
+    loss = torch.zeros(1, dtype=torch.float64, device="cuda")
+    scr = ev.loss_scratch[0]
+    for slot, want_nan in ((1, False), (2, True), (5, True)):
+        _lib.check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][0].data_ptr(), sl["geoms"][0].numel(),
+                                                binning.data_ptr(), binning.numel(), N, slot, 6, ev.gts[0].data_ptr(),
+                                                None, scr.data_ptr(), scr.numel() * 8, loss.data_ptr(), 0,
+                                                _lib.stream_handle()))
+        v = float(loss)
+        assert math.isnan(v) == want_nan, (slot, v)

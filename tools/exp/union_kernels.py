@@ -70,27 +70,27 @@ def pre():
 
 
 def ugeo():
-    check(lib.gslm_union_geometry(ctypes.byref(vw), P, ge, n, ugeom.data_ptr(), nb, st))
+    check(lib.gslm_union_geometry(ctypes.byref(vw), P, ge, n, nb, ugeom.data_ptr(), nb, st))
 
 
 def ubin():
     N = box["N"]
     check(lib.gslm_union_binning(ctypes.byref(vw), P, ugeom.data_ptr(), box["bin"].data_ptr(), box["bin"].numel(), N, ge,
-                                 n, st))
+                                 n, nb, st))
 
 
 def blends():
     N = box["N"]
     for k in range(n):
-        check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, geoms[k].data_ptr(), box["bin"].data_ptr(),
-                                           box["bin"].numel(), N, k, gt.data_ptr(), None, scr.data_ptr(), scr.numel() * 8,
+        check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, geoms[k].data_ptr(), nb, box["bin"].data_ptr(),
+                                           box["bin"].numel(), N, k, n, gt.data_ptr(), None, scr.data_ptr(), scr.numel() * 8,
                                            losses.data_ptr() + 8 * k, 0, st))
 
 
 def blend_sets():
     N = box["N"]
     lp = (ctypes.c_void_p * n)(*[losses.data_ptr() + 8 * k for k in range(n)])
-    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, box["bin"].data_ptr(), box["bin"].numel(), N,
+    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, nb, box["bin"].data_ptr(), box["bin"].numel(), N,
                                        gt.data_ptr(), None, scr.data_ptr(), scr.numel() * 8, lp, 0, st))
 
 
