@@ -505,14 +505,17 @@ size_t gslm_loss_sets_scratch_bytes(int32_t n, int32_t H, int32_t W) {
   return (size_t)(n > 0 ? n : 1) * gslm_loss_scratch_bytes(H, W);
 }
 
-int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
-                             const void* binning, size_t binning_bytes, int64_t N, const float* gt,
+int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, int32_t first_set,
+                             size_t set_bytes, const void* binning, size_t binning_bytes, int64_t N, const float* gt,
                              const float* alpha_mask, void* scratch, size_t scratch_bytes, double* const* loss_dev,
                              int32_t accumulate, void* stream) {
   ViewK v;
   int st = make_view(view, 1, &v);
   if (st) return st;
-  if (n < 1 || n > MAX_UNION_SETS) { set_error("rasterize_loss_sets: 1 <= n <= 8 parameter sets"); return GSLM_ERR_INVALID; }
+  if (n < 1 || first_set < 0 || first_set + n > MAX_UNION_SETS) {
+    set_error("rasterize_loss_sets: 1 <= n parameter sets, slots first_set .. first_set + n - 1 within [0, 8)");
+    return GSLM_ERR_INVALID;
+  }
   if (N < 0 || N > 0xFFFFFFFFll) { set_error("rasterize_loss_sets: N out of range"); return GSLM_ERR_INVALID; }
   if (binning_bytes < gslm_union_binning_bytes(N, v.H, v.W) || !binning) { set_error("union binning workspace too small"); return GSLM_ERR_CAPACITY; }
   if (scratch_bytes < gslm_loss_sets_scratch_bytes(n, v.H, v.W)) { set_error("loss scratch too small"); return GSLM_ERR_CAPACITY; }
@@ -532,7 +535,7 @@ int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const
   bin_layout(N, v.gx * v.gy, const_cast<void*>(binning), &bb);
   union_masks_layout(N, v.gx * v.gy, const_cast<void*>(binning), &um);
   return launch_render_loss_sets(v, sr, n, bb, um.sorted, gt, alpha_mask, (double*)scratch, lp, accumulate ? 1 : 0,
-                                 (hipStream_t)stream);
+                                 (hipStream_t)stream, first_set);
 }
 
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream) {

@@ -10,6 +10,10 @@
 #include "gslm_chain.hpp"
 #include "gslm_gather.hpp"
 
+#ifndef GSLM_BWD_FILL
+#define GSLM_BWD_FILL 1
+#endif
+
 namespace gslm {
 
 // ROWF4 = 3: drop-in rows (screen position and inverse depth too); ROWF4 = 2: the LM rows of
@@ -26,8 +30,10 @@ __global__ __launch_bounds__(256, 8) void k_render_bwd(ViewK v, const uint2* __r
                                                      const float* __restrict__ dL_dcolor,
                                                      const float* __restrict__ dL_dinv, float4* __restrict__ rows,
                                                      int write_tail) {
-  // 128-entry batches (as k_render_matvec): 24-26 KB of LDS per block -> 6 blocks per CU
-  constexpr int B = 128;
+  // 128-entry batches for the LM rows (as k_render_matvec: 19.7 KB of LDS); 96 for the drop-in's 9-10 values per row,
+  // whose partials at 128 entries took 24-26 KB of LDS per block -> 6 blocks per CU, at 96 entries 17.9-19.5 KB -> 8
+  // blocks per CU, and under __launch_bounds__(256, 8) 44-45 VGPRs (74-76 without the hint): 8 waves per SIMD
+  constexpr int B = WITH_XY ? 96 : 128;
   __shared__ float4 s_r0[B], s_r1[B];
   __shared__ float2 s_r2[B];
   __shared__ uint64_t s_bits[16];
@@ -63,14 +69,23 @@ int launch_render_bwd(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, con
                       const float* dL_dcolor, const float* dL_dinv, const ScratchBufs& sb, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
   if (N == 0) return GSLM_OK;
+  // every (tile, Gaussian) row zero first -- a streaming fill -- and the tile pass writes only the rows of entries some
+  // wave visits (until round 5 it wrote every row, the never-blended ones as zeros through the rectangle's row slot:
+  // three dependent random loads and a scattered 48-B store per entry, for about half of the list)
+#if GSLM_BWD_FILL
+  GSLM_HIP_CHECK(hipMemsetAsync(sb.contrib, 0, (size_t)N * 3 * sizeof(float4), s));
+  constexpr int write_tail = 0;
+#else
+  constexpr int write_tail = 1;
+#endif
   if (dL_dinv)
     hipLaunchKernelGGL((k_render_bwd<true, true, 3>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv,
-                       sb.contrib, 1);
+                       sb.contrib, write_tail);
   else
     hipLaunchKernelGGL((k_render_bwd<true, false, 3>), dim3(ntiles), dim3(TILE_PIX), 0, s, v, bb.ranges, bb.tile_order,
                        bb.point_list, gb.rec, nullptr, gb.rect, gb.goff, ib.final_T, ib.n_contrib, dL_dcolor, dL_dinv,
-                       sb.contrib, 1);
+                       sb.contrib, write_tail);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

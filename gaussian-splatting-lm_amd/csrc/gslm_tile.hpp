@@ -223,10 +223,12 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       s_r1[tid] = rec[RECS * (int64_t)g + 1];
       const float4 r2 = rec[RECS * (int64_t)g + 2];
       s_r2[tid] = make_float2(r2.x, r2.y);
-      my_slot = slots ? slots[range.x + base - tid] : row_slot(goff[g], rect[g], tile_x, tile_y);
       // and only the waves that still blend at this list position
       const int pos = base - tid;
       my_mask &= (pos < wm0 ? 1u : 0u) | (pos < wm1 ? 2u : 0u) | (pos < wm2 ? 4u : 0u) | (pos < wm3 ? 8u : 0u);
+      // the row slot of an entry that gets a row (below): the LM row map, or the drop-in's rectangle slot
+      if (my_mask || (!slots && write_tail))
+        my_slot = slots ? slots[range.x + base - tid] : row_slot(goff[g], rect[g], tile_x, tile_y);
     }
     // which waves' quadrants this element can touch; wave w visits only its hits, and the combine below
     // takes zero for the others (exactly what a visit with no valid lane would have produced)
@@ -285,9 +287,11 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           // and their constant factors (-1/2, -1, -1/2) are applied once per row at the combine
           const float h = b.y * gv[5];
           const float hdx = h * dx, hdy = h * dy;
+          // the screen-position rows: the conic is the entry's, so dL/dx = -(A sum h dx + B sum h dy) and dL/dy =
+          // -(C sum h dy + B sum h dx) are formed from the two sums once per row at the combine (not per lane)
           if (WITH_XY) {
-            gv[0] = -(hdx * a.z + hdy * a.w);
-            gv[1] = -(hdy * b.x + hdx * a.w);
+            gv[0] = hdx;
+            gv[1] = hdy;
           }
           gv[2] = hdx * dx;
           gv[3] = hdx * dy;
@@ -337,7 +341,10 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       }
     }
     __syncthreads();
-    if (tid < cnt && (!slots || my_mask)) {  // LM rows (slots): head entries only, see k_row_flags
+    // rows only for the entries some wave visited: the LM rows (slots) exist for head entries only (k_row_flags); the
+    // drop-in's rectangle rows of every other entry are the zeros its caller filled the buffer with (write_tail = 0),
+    // or were written by the tail loop above (write_tail)
+    if (tid < cnt && (my_mask || (!slots && write_tail))) {
       float t[NV];
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
@@ -358,6 +365,12 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       t[2] *= -0.5f;  // the conic rows' constant factors (see the hit loop)
       t[3] = -t[3];
       t[4] *= -0.5f;
+      if (WITH_XY) {  // sum h dx, sum h dy -> dL/d(x, y) with the entry's conic (A, B, C)
+#pragma clang fp contract(fast)
+        const float cA = s_r0[tid].z, cB = s_r0[tid].w, cC = s_r1[tid].x, sx = t[0], sy = t[1];
+        t[0] = -(cA * sx + cB * sy);
+        t[1] = -(cC * sy + cB * sx);
+      }
       store_row<ROWF4>(rows, my_slot, t);
     }
   }

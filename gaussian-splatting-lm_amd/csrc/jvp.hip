@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void k_render_jvp(ViewK v, const uint2* __rest
 
 // Fused (J^T W J) v for one view: JVP pass, per-pixel weight, VJP pass.
 template <bool WITH_XY>
-__global__ __launch_bounds__(256, 8) void k_render_matvec(ViewK v, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(256, WITH_XY ? 6 : 8) void k_render_matvec(ViewK v, const uint2* __restrict__ ranges,
                                                         const uint32_t* __restrict__ tile_order,
                                                         const uint32_t* __restrict__ point_list,
                                                         const float4* __restrict__ rec, const float4* __restrict__ trec,

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
                                                            const uint32_t* __restrict__ point_list,
                                                            const uint32_t* __restrict__ amask, SetRecsK sr,
                                                            const float* __restrict__ gt, const float* __restrict__ mask,
-                                                           double* __restrict__ part) {
+                                                           double* __restrict__ part, int shift) {
   __shared__ float4 s_rec[4][3 * 64];
   const int tile = (int)tile_order[blockIdx.x];
   const int tile_x = tile % v.gx, tile_y = tile / v.gx;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
     uint32_t g = 0u, m = 0u;
     if (k < n) {
       g = pl_id(pl[k]);
-      m = am[k];
+      m = am[k] >> shift;  // sets first_set.. of the union binning (gslm_rasterize_loss_sets' first_set)
     }
     // set 0's records of this lane's entry (if it is a hit of a set still blending)
     bool hit = dmask[0] != ~0ull && ((m >> q) & 1u);
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __re
 
 int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const BinBufs& bb, const uint32_t* amask,
                             const float* gt, const float* mask, double* part, const LossPtrsK& lp, int accumulate,
-                            hipStream_t s) {
+                            hipStream_t s, int first_set) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) {
     if (!accumulate)
@@ -293,7 +293,7 @@ int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const
 #define GSLM_LOSS_SETS(NS)                                                                                           \
   case NS:                                                                                                           \
     hipLaunchKernelGGL(k_render_loss_sets<NS>, grid, block, 0, s, v, bb.ranges, bb.tile_order, bb.point_list, amask, \
-                       sr, gt, mask, part);                                                                          \
+                       sr, gt, mask, part, 4 * first_set);                                                           \
     break;
     GSLM_LOSS_SETS(1) GSLM_LOSS_SETS(2) GSLM_LOSS_SETS(3) GSLM_LOSS_SETS(4)
     GSLM_LOSS_SETS(5) GSLM_LOSS_SETS(6) GSLM_LOSS_SETS(7) GSLM_LOSS_SETS(8)

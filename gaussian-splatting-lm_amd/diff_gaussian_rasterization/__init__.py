@@ -142,6 +142,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         color, radii, invdepth, geom, binning, image, nr = output
         ctx.raster_settings = raster_settings
         ctx.num_rendered = int(nr.item())
+        # outputs the loss does not use reach backward as None, not as zero tensors: an unused inverse depth (the
+        # reference's LM residual never reads it) then runs the backward without its gradient slot (9 values per row
+        # instead of 10) and allocates no [1, H, W] of zeros
+        ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(radii, geom, binning, image, nr)
         saved = (means3D, sh, dc, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, geom, binning, image)
         ctx.save_for_backward(*saved)

@@ -129,7 +129,8 @@ EXPORTS = {
                                                 ctypes.c_void_p]),
     "gslm_loss_sets_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "gslm_rasterize_loss_sets": (ctypes.c_int, [ctypes.POINTER(GslmView), ctypes.c_int64,
-                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.c_size_t,
                                                 ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p]),

@@ -852,11 +852,13 @@ class LossEvaluator:
         self.uslots = [[dict(geoms=[], ugeom=None) for _ in range(self.batch)] for _ in range(2)]
         self.ubins = [None] * self.batch
         self.sets_scratch = [None] * self.batch
-        # the six points' blends: one pass per set over each union list (gslm_rasterize_loss_slot), or one pass for all
-        # sets (gslm_rasterize_loss_sets; GSLM_LOSS_SETS=1) -- the same losses bitwise.  Per set is the default: the
-        # all-sets pass wins when evaluate_points runs back to back (69.8 against 74.8 ms for the six points over 50
-        # views) but loses inside lm_step (LM step 98.3 against 95.5 ms, same box; profiles/r04/ab/all_sets_default/)
-        self.loss_sets = os.environ.get("GSLM_LOSS_SETS", "0") == "1"
+        # the six points' blends: one pass per set over each union list (gslm_rasterize_loss_slot; loss_sets = 1), or
+        # passes over groups of loss_sets sets each (gslm_rasterize_loss_sets) -- the same losses bitwise.  Per set is
+        # the default: the all-sets pass wins when evaluate_points runs back to back (69.8 against 74.8 ms for the six
+        # points over 50 views) but not inside lm_step, where it holds the CUs longer against the next batch's sorts
+        # on the other streams (profiles/r04/ab/all_sets_default/, profiles/r05/ab/loss_set_groups/).  GSLM_LOSS_SETS=k
+        # selects groups of k (1 = per set; the round-4 GSLM_LOSS_SETS=1 meaning "all sets" is k = 8).
+        self.loss_sets = max(1, min(8, int(os.environ.get("GSLM_LOSS_SETS", "1"))))
         self.union_counts = []
 
     def _slot(self, k, P):
@@ -1117,13 +1119,17 @@ class LossEvaluator:
                 check(lib.gslm_union_binning(ctypes.byref(vw), P, sl["ugeom"].data_ptr(), binning.data_ptr(),
                                              binning.numel(), N, ge, n, sb, sh), "gslm_union_binning")
                 m = self.masks[i]
-                if self.loss_sets:  # all sets in one pass over the union list
-                    scr = self._sets_scratch(k, n, H, W)
-                    lp = (ctypes.c_void_p * n)(*[losses[a].data_ptr() + 8 * i for a in range(n)])
-                    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, sb, binning.data_ptr(), binning.numel(), N,
-                                                       self.gts[i].data_ptr(), None if m is None else m.data_ptr(),
-                                                       scr.data_ptr(), scr.numel() * 8, lp, 0, sh),
-                          "gslm_rasterize_loss_sets")
+                if self.loss_sets > 1:  # groups of loss_sets sets, one pass over the union list each
+                    gsz = min(self.loss_sets, n)
+                    scr = self._sets_scratch(k, gsz, H, W)
+                    for a0 in range(0, n, gsz):
+                        na = min(gsz, n - a0)
+                        gg = (ctypes.c_void_p * na)(*[sl["geoms"][a].data_ptr() for a in range(a0, a0 + na)])
+                        lp = (ctypes.c_void_p * na)(*[losses[a].data_ptr() + 8 * i for a in range(a0, a0 + na)])
+                        check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, gg, na, a0, sb, binning.data_ptr(),
+                                                           binning.numel(), N, self.gts[i].data_ptr(),
+                                                           None if m is None else m.data_ptr(), scr.data_ptr(),
+                                                           scr.numel() * 8, lp, 0, sh), "gslm_rasterize_loss_sets")
                     continue
                 scr = self.loss_scratch[k % len(self.streams)]
                 for a in range(n):

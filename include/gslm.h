@@ -202,14 +202,15 @@ int gslm_rasterize_loss_slot(const gslm_view* view, int64_t P, const void* geom,
                              size_t binning_bytes, int64_t num_rendered, int32_t slot, int32_t n_sets, const float* gt,
                              const float* alpha_mask, void* scratch, size_t scratch_bytes, double* loss_dev,
                              int32_t accumulate, void* stream);
-/* Step 4 for all n sets in one pass over the union list (the list walked once; set a + 1's records loaded while set
- * a's hits are visited): *loss_dev[a] = [*loss_dev[a] if accumulate] + set a's loss, bitwise each
- * gslm_rasterize_loss_slot(geoms[a], a).  scratch >= gslm_loss_sets_scratch_bytes(n, H, W). */
+/* Step 4 for n sets in one pass over the union list (the list walked once; set a + 1's records loaded while set a's
+ * hits are visited): geoms[a] / loss_dev[a] are slot first_set + a's (ABI 9: a group of the binning's sets);
+ * *loss_dev[a] = [*loss_dev[a] if accumulate] + that set's loss, bitwise gslm_rasterize_loss_slot(geoms[a],
+ * first_set + a).  scratch >= gslm_loss_sets_scratch_bytes(n, H, W). */
 size_t gslm_loss_sets_scratch_bytes(int32_t n, int32_t H, int32_t W);
-int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, size_t set_bytes,
-                             const void* binning, size_t binning_bytes, int64_t num_rendered, const float* gt,
-                             const float* alpha_mask, void* scratch, size_t scratch_bytes, double* const* loss_dev,
-                             int32_t accumulate, void* stream);
+int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const* geoms, int32_t n, int32_t first_set,
+                             size_t set_bytes, const void* binning, size_t binning_bytes, int64_t num_rendered,
+                             const float* gt, const float* alpha_mask, void* scratch, size_t scratch_bytes,
+                             double* const* loss_dev, int32_t accumulate, void* stream);
 /* Convenience: gslm_preprocess + gslm_num_rendered + gslm_rasterize.  If binning_bytes is too
  * small returns GSLM_ERR_CAPACITY with *out_num_rendered set (geometry is valid: call
  * gslm_rasterize with a larger buffer). */

@@ -274,14 +274,16 @@ def test_fullsize_backward_whole_frame_100k():
     got = {k: v.grad.cpu() for k, v in ag.items()} | {"means2D": m2g.grad.cpu()}
     # over the whole frame a handful of (entry, pixel) alpha tests sit within an ulp of the 1/255 cut, where the GPU's
     # v_exp_f32 and the oracle's exp decide differently (the forward's flipped pixels above): each moves the gradients
-    # of the Gaussians behind that pixel, so the max-based error is set by the worst flip (round 4: 7.6e-5 of the max
-    # for the SH gradient, 1.7e-4 for means3D under one extra exponent rounding).  Asserted: the error over every
-    # Gaussian (L2, rel 1e-5) and, per element, a flip-sized guard (5e-4 of the max).
+    # of the Gaussians behind that pixel, so the max-based error is set by the worst flip.  Measured (round 5,
+    # profiles/r05/parity_margins*.jsonl): the kept kernels 3.8e-6 L2 / 7.6e-5 per element (SH gradient, the worst);
+    # round 4's rejected log2e-prescaled exponent -- one more rounding in every alpha -- 2.1e-5 / 3.8e-4 (scales).  A
+    # wrong derivative is O(1).  Asserted: the error over every Gaussian (L2 rel 5e-5) and, per element, a flip-sized
+    # guard (1e-3 of the max); until round 5 a per-element 1e-4, which that one rounding broke (1.7e-4).
     for k in ref:
         T = "test_fullsize_backward_whole_frame_100k"
-        l2 = record(T, f"grad {k} (L2 rel)", _l2_rel(got[k], ref[k]), 1e-5)
-        err = record(T, f"grad {k} (of max, per element)", _rel_err(got[k], ref[k]), 5e-4)
-        assert l2 <= 1e-5 and err < 5e-4, f"grad {k}: L2 {l2:.3e}, max {err:.3e}"
+        l2 = record(T, f"grad {k} (L2 rel)", _l2_rel(got[k], ref[k]), 5e-5)
+        err = record(T, f"grad {k} (of max, per element)", _rel_err(got[k], ref[k]), 1e-3)
+        assert l2 <= 5e-5 and err < 1e-3, f"grad {k}: L2 {l2:.3e}, max {err:.3e}"
 
 
 def test_fullsize_lm_matvec_whole_frame_100k():

@@ -76,10 +76,12 @@ def test_evaluate_points_equal_exact_renders(batch, streams):
     for i, N in enumerate(ev_u.union_counts):
         assert N >= max(c[i] for c in counts)
     assert any(N > min(c[i] for c in counts) for i, N in enumerate(ev_u.union_counts))
-    # the per-set blends (one pass per set) give the same losses as the all-sets pass
-    ev_u.loss_sets = False
-    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
-    ev_u.loss_sets = True
+    # the blends over groups of sets (all sets in one pass; pairs and triples, with a ragged last group) give the same
+    # losses as the per-set blends (the default)
+    for k in (8, 2, 4):
+        ev_u.loss_sets = k
+        assert [float(x) for x in ev_u.evaluate_points(sets)] == exact, k
+    ev_u.loss_sets = 3
     # fewer points, and a second LM step on the same evaluator (buffers reused, depth orders cached)
     assert [float(x) for x in ev_u.evaluate_points(sets[2:5])] == exact[2:5]
     sets2, exact2, _, _ = _points(m, lay, s, ev_x)
@@ -97,7 +99,7 @@ def test_evaluate_points_equal_exact_renders_low_sh_degree(D):
     ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=2, streams=2)
     sets, exact, _, _ = _points(m, lay, s, ev_x)
     assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
-    ev_u.loss_sets = False
+    ev_u.loss_sets = 8
     assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
 
 

@@ -93,10 +93,10 @@ def timed(fn):
 if a.mode in ("both", "exact"):
     out["exact_6_points_ms"] = timed(lambda: [ev_x.evaluate() for _ in range(6)])
 if a.mode in ("both", "union"):
-    ev_u.loss_sets = False
+    ev_u.loss_sets = 1
     out["union_6_points_ms"] = timed(lambda: ev_u.evaluate_points(sets))  # the default: per-set blends
-    ev_u.loss_sets = True
+    ev_u.loss_sets = 8
     out["union_6_points_all_sets_blend_ms"] = timed(lambda: ev_u.evaluate_points(sets))
-    ev_u.loss_sets = False
+    ev_u.loss_sets = 1
     out["snapshot_ms"] = timed(lambda: [param_snapshot(model) for _ in range(6)])
 print(json.dumps(out), flush=True)

@@ -90,7 +90,7 @@ def blends():
 def blend_sets():
     N = box["N"]
     lp = (ctypes.c_void_p * n)(*[losses.data_ptr() + 8 * k for k in range(n)])
-    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, nb, box["bin"].data_ptr(), box["bin"].numel(), N,
+    check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, ge, n, 0, nb, box["bin"].data_ptr(), box["bin"].numel(), N,
                                        gt.data_ptr(), None, scr.data_ptr(), scr.numel() * 8, lp, 0, st))
 
 
