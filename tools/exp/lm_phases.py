@@ -16,6 +16,7 @@ import torch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--P", type=int, default=1_000_000)
+ap.add_argument("--val-batch", type=int, default=8, help="lm_step's val_batch (1: one stream, solo kernel times)")
 ap.add_argument("--copy-xyz", action="store_true", help="restore xyz too between steps (drops the cached depth orders)")
 a = ap.parse_args()
 from gslm.cameras import orbit_cameras  # noqa: E402
@@ -52,19 +53,19 @@ def restore():
 
 
 out = {"copy_xyz": a.copy_xyz, "untimed_ms": [], "timed": []}
-lm_step(model, cams, val, bg, max_iter=10, restart_iter=10)
+lm_step(model, cams, val, bg, max_iter=10, restart_iter=10, val_batch=a.val_batch)
 restore()
 for _ in range(a.reps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lm_step(model, cams, val, bg, max_iter=10, restart_iter=10)
+    lm_step(model, cams, val, bg, max_iter=10, restart_iter=10, val_batch=a.val_batch)
     torch.cuda.synchronize()
     out["untimed_ms"].append(round(1e3 * (time.perf_counter() - t0), 2))
     restore()
 for _ in range(a.reps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    o = lm_step(model, cams, val, bg, max_iter=10, restart_iter=10, timing=True)
+    o = lm_step(model, cams, val, bg, max_iter=10, restart_iter=10, timing=True, val_batch=a.val_batch)
     wall = 1e3 * (time.perf_counter() - t0)
     restore()
     out["timed"].append({"wall_ms": round(wall, 2), **{k: round(v, 2) for k, v in o["timing"].items()}})

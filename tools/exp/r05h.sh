@@ -13,3 +13,5 @@ for r in 1 2; do
     echo "k=$k r=$r $(tail -c 400 $O/lm_k${k}_r$r.json)"
   done
 done
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+tail -c 3000 $O/bench.json
