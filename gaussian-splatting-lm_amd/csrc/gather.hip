@@ -50,14 +50,19 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
   }
   const int nc = (v.D + 1) * (v.D + 1);
   const bool sh_out = !g.colors && (out.dc || out.rest);
+  // the SH colour's view-direction term of the means gradient needs <dres, sh_k> for every coefficient: per thread at a
+  // 3M-float stride each of those 3(nc - 1) loads touches a line per lane, so it is formed block-cooperatively below
+  // from coalesced reads of the block's SH rows (DEFER_DIR; block-uniform)
+  const bool dir_term = want_means && out.means3D && !g.colors && v.D > 0;
   ChainOut co;
   if (i < g.P) {
-    chain_vjp<RAW>(v, g, i, n != 0, n ? clampw[i] : 0u, G2, want_means != 0, co);
-    write_grads(g, out, i, co, v.M, nc, want_means != 0, /*skip_sh=*/true);
+    chain_vjp<RAW, true>(v, g, i, n != 0, n ? clampw[i] : 0u, G2, want_means != 0, co);
+    write_grads(g, out, i, co, v.M, nc, want_means != 0 && !dir_term, /*skip_sh=*/true);
   }
-  if (!sh_out) return;  // block-uniform
+  if (!sh_out && !dir_term) return;  // block-uniform
   // factored staging (gslm_gather.hpp): dsh[k][ch] = shB[k] dres[ch]
   float* s_d = s_buf + 256 * SHB_STRIDE;
+  float* s_w = s_d + 256 * 4;  // [256][SHB_STRIDE]: <dres, sh_k> of the block's Gaussians
   if (i < g.P) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) s_buf[tid * SHB_STRIDE + k] = co.shB[k];
@@ -65,6 +70,30 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(ViewK v, GaussK g, const
     for (int ch = 0; ch < 3; ++ch) s_d[tid * 4 + ch] = co.dres[ch];
   }
   __syncthreads();
+  if (dir_term) {
+    // element e = (Gaussian ii, coefficient k): 64 lanes read 4 Gaussians' consecutive 48-float rows
+    for (int e = tid; e < (int)nvalid * 16; e += blockDim.x) {
+      const int ii = e >> 4, k = e & 15;
+      float w = 0.f;
+      if (k >= 1 && k < nc) {
+        const int64_t gi = i0 + ii;
+        const float s0 = g.sh(gi, k, 0), s1 = g.sh(gi, k, 1), s2 = g.sh(gi, k, 2);
+        w = s_d[ii * 4 + 0] * s0 + s_d[ii * 4 + 1] * s1 + s_d[ii * 4 + 2] * s2;  // chain_vjp's w, bitwise
+      }
+      s_w[ii * SHB_STRIDE + k] = w;
+    }
+    __syncthreads();
+    if (i < g.P && n != 0) {
+      float dm[3] = {co.dmean[0], co.dmean[1], co.dmean[2]};
+      add_dir_term(v.D, co.dir, co.dirlen, s_w + tid * SHB_STRIDE, dm);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) put(&out.means3D[3 * i + k], dm[k], out.accumulate);
+    } else if (i < g.P) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) put(&out.means3D[3 * i + k], co.dmean[k], out.accumulate);
+    }
+  }
+  if (!sh_out) return;
   const int acc = out.accumulate;
   const int R = 3 * v.M;
   const float invR = 1.0f / (float)R;
@@ -184,10 +213,12 @@ int launch_preprocess_bwd(const ViewK& v, const GaussK& g, const GeomBufs& gb, c
   (void)bb;
   if (g.P == 0) return GSLM_OK;
   const unsigned nb = (unsigned)((g.P + 255) / 256);
-  const size_t sh_lds = sh_stage_floats<true>(g.M) * sizeof(float);
+  // the factored SH stage and the block's <dres, sh_k> (256 x SHB_STRIDE floats)
+  const size_t sh_lds = (sh_stage_floats<true>(g.M) + (size_t)256 * SHB_STRIDE) * sizeof(float);
   const size_t chunk_lds = (size_t)GATHER_CHUNK * 3 * sizeof(float4);
   // (staging the primal SH rows here as k_preprocess_jvp does measured 221 -> 229 us at 1M: the 48 KB of LDS cost
-  // more occupancy than the strided reads; profiles/r04/ab/dropin_staging)
+  // more occupancy than the strided reads; profiles/r04/ab/dropin_staging -- only the 15 dot products with dres
+  // are needed, formed from coalesced reads instead)
   const size_t lds = sh_lds > chunk_lds ? sh_lds : chunk_lds;
   if (g.raw)
     hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3(nb), dim3(256), lds, s, v, g, gb.clampw, gb.tiles, gb.goff,

@@ -116,10 +116,16 @@ struct ChainOut {
   // per-Gaussian epilogues stage these 19 floats instead of the 3M products
   float shB[16];
   float dres[3];
+  // DEFER_DIR: the view direction (unit) and its length, for the SH colour's view-direction term of dmean that the
+  // caller adds itself (add_dir_term)
+  float dir[3];
+  float dirlen;
 };
 
 // Reverse mode: G2 = reduced screen-space gradient [x_pix, y_pix, conic a, b, c, opacity_eff, r, g, b, invdepth].
-template <bool RAW>
+// DEFER_DIR: dmean leaves out the SH colour's view-direction term, sum_k dB_k/ddir <dres, sh_k> (the only use of the
+// primal SH coefficients), and co.dir / co.dirlen are set for the caller's add_dir_term.
+template <bool RAW, bool DEFER_DIR = false>
 __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64_t i, bool visible,
                                           uint32_t clamped, const float G2[10], bool want_means, ChainOut& co) {
   co.dm2[0] = co.dm2[1] = 0.f;
@@ -277,7 +283,11 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
     for (int j = 0; j < 3; ++j)
       co.dmean[j] += (pm[4 * j + 0] * e.p_w - pm[4 * j + 3] * mul1) * gpx + (pm[4 * j + 1] * e.p_w - pm[4 * j + 3] * mul2) * gpy;
     // view direction of the SH colour
-    if (!g.colors && v.D > 0) {
+    if (DEFER_DIR) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) co.dir[j] = e.dir[j];
+      co.dirlen = e.dirlen;
+    } else if (!g.colors && v.D > 0) {
       float dB[16][3];
       sh_basis_grad(v.D, e.dir[0], e.dir[1], e.dir[2], dB);
       float ddir[3] = {0.f, 0.f, 0.f};
@@ -297,6 +307,25 @@ __device__ __forceinline__ void chain_vjp(const ViewK& v, const GaussK& g, int64
     }
   }
   co.dop = RAW ? dop_act * e.op * (1.f - e.op) : dop_act;
+}
+
+// chain_vjp's view-direction term of dmean from w[k] = <dres, sh_k> (k = 1 .. nc - 1): the same operations in the
+// same order, so the same dmean bitwise.
+__device__ __forceinline__ void add_dir_term(int D, const float dir[3], float dirlen, const float* w, float dmean[3]) {
+  float dB[16][3];
+  sh_basis_grad(D, dir[0], dir[1], dir[2], dB);
+  float ddir[3] = {0.f, 0.f, 0.f};
+  const int nc = (D + 1) * (D + 1);
+#pragma unroll
+  for (int k = 1; k < 16; ++k)
+    if (k < nc) {
+      const float wk = w[k];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ddir[j] += dB[k][j] * wk;
+    }
+  const float dd = dir[0] * ddir[0] + dir[1] * ddir[1] + dir[2] * ddir[2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dmean[j] += (ddir[j] - dir[j] * dd) / dirlen;
 }
 
 __device__ __forceinline__ void put(float* p, float v, int acc) {
