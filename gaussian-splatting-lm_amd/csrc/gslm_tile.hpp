@@ -283,10 +283,10 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           const float dL_dalpha = cd_acc * st.T + st.tb * inv1ma;
           st.accd = st.accd + a_e * cd_acc;  // this Gaussian joins the accumulation behind the next one
           gv[5] = G_e * dL_dalpha;
-          // h = G dL/dG with G = exp(power): dL/dpower = h; the conic rows carry h dx^2, h dx dy, h dy^2
-          // and their constant factors (-1/2, -1, -1/2) are applied once per row at the combine
-          const float h = b.y * gv[5];
-          const float hdx = h * dx, hdy = h * dy;
+          // h = G dL/dG = o gv5 with G = exp(power): dL/dpower = h; the conic rows carry gv5 dx^2, gv5 dx dy,
+          // gv5 dy^2 and their factors o (-1/2, -1, -1/2) are applied once per row at the combine (the entry's
+          // opacity o is the same at every pixel: one VALU less per visit)
+          const float hdx = gv[5] * dx, hdy = gv[5] * dy;
           // the screen-position rows: the conic is the entry's, so dL/dx = -(A sum h dx + B sum h dy) and dL/dy =
           // -(C sum h dy + B sum h dx) are formed from the two sums once per row at the combine (not per lane)
           if (WITH_XY) {
@@ -305,10 +305,11 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
 #pragma unroll
             for (int q = 0; q < NV; ++q)
               if (q_used<WITH_XY, WITH_INV>(q)) pv[q_slot<WITH_XY, WITH_INV>(q)] = gv[q];
-            // unused slots (7 with the LM rows) are never stored: any register will do, and slot k - 4 pairs
-            // with it in the first permlane step anyway (no zero materialised per visit)
+            // unused slots (7 with the LM rows) are never stored and never mix into a stored one (slot k + 4 stays in
+            // the other half-wave through every step): any register will do -- a dead one (dy), which the permlane swap
+            // may overwrite in place; an alias of a live slot cost a copy per visit
 #pragma unroll
-            for (int k = NU; k < 8; ++k) pv[k] = pv[k - 4];
+            for (int k = NU; k < 8; ++k) pv[k] = k == 7 ? dy : pv[k - 4];
             rr = wave_reduce8_t(pv, lane);
           }
           const int k = lane >> 3;
@@ -362,12 +363,14 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
           t[q] = ((p0 + p1) + p2) + p3;
         }
       }
-      t[2] *= -0.5f;  // the conic rows' constant factors (see the hit loop)
-      t[3] = -t[3];
-      t[4] *= -0.5f;
-      if (WITH_XY) {  // sum h dx, sum h dy -> dL/d(x, y) with the entry's conic (A, B, C)
+      // the conic rows' factors o (-1/2, -1, -1/2) (see the hit loop)
+      const float op = s_r1[tid].y;
+      t[2] *= -0.5f * op;
+      t[3] *= -op;
+      t[4] *= -0.5f * op;
+      if (WITH_XY) {  // o sum gv5 dx, o sum gv5 dy -> dL/d(x, y) with the entry's conic (A, B, C)
 #pragma clang fp contract(fast)
-        const float cA = s_r0[tid].z, cB = s_r0[tid].w, cC = s_r1[tid].x, sx = t[0], sy = t[1];
+        const float cA = s_r0[tid].z, cB = s_r0[tid].w, cC = s_r1[tid].x, sx = op * t[0], sy = op * t[1];
         t[0] = -(cA * sx + cB * sy);
         t[1] = -(cC * sy + cB * sx);
       }
