@@ -34,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "CG matvecs/sec + raster Mpix/s, 1M Gaussians @1080p, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+RASTER_STREAMS = 4  # renders in flight for the multi-stream raster throughput (`raster_streams` in the line)
 
 
 def parse():
@@ -301,6 +302,37 @@ def main():
     barrier()
     t_fwd_sync = max_over_ranks(time.perf_counter() - t0)  # (leaves every view in forward()'s exact layout)
     mpix_sync = n_views * W * H * fsteps / t_fwd_sync / 1e6
+    # the same device-count forwards with RASTER_STREAMS renders in flight on as many HIP streams (the line search's
+    # setting: independent validation renders overlap, a render's launch-bound sort passes beside another's blend) --
+    # a throughput over many renders, reported beside the one-stream rate above, which stays `raster_mpix_s`
+    raster_streams = None
+    if not args.no_side and prob.views:
+        from gslm.lm import ViewRaster
+        S = RASTER_STREAMS
+        vr0 = prob.views[0]
+        rasters = [ViewRaster(vr0.view, device) for _ in range(S)]
+        streams = [torch.cuda.Stream(device) for _ in range(S)]
+        for r, st in zip(rasters, streams):
+            r.forward(graw, st.cuda_stream)
+        capz = [r.capacity() for r in rasters]
+        cnt_s = torch.zeros(max(fsteps, 1) * S, dtype=torch.int32, device=device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(fsteps):
+            for j, (r, st) in enumerate(zip(rasters, streams)):
+                r.forward_dev(graw, st.cuda_stream, n_out=cnt_s.data_ptr() + 4 * (it * S + j))
+        torch.cuda.synchronize()
+        t_s = time.perf_counter() - t0
+        cs = cnt_s.view(max(fsteps, 1), S).tolist()
+        if any(c[j] > capz[j] for c in cs[:fsteps] for j in range(S)):
+            raise RuntimeError("raster_streams: a pair count exceeded its list capacity")
+        raster_streams = {"streams": S, "renders": S * fsteps, "mpix_s": S * fsteps * W * H / t_s / 1e6,
+                          "ms_per_render": 1e3 * t_s / (S * fsteps),
+                          "note": f"{S} independent forwards of view 0 in flight on {S} HIP streams (gslm_rasterize_dev, "
+                                  "counts checked after the loop): render throughput, not one forward's latency "
+                                  "(raster_mpix_s / forward_ms_per_view)"}
+        del rasters, streams
+        torch.cuda.empty_cache()
 
     # ---------------- roofline of the dominant kernel: the fused JVP->VJP tile pass (k_render_matvec)
     loc = getattr(prob, "local", prob)  # the rank's own LMProblem (full P) under a sharded operator
@@ -468,6 +500,7 @@ def main():
             "raster_sync": {"mpix_s": mpix_sync, "forward_ms_per_view": 1e3 * t_fwd_sync / fsteps / max(n_views_local, 1),
                             "note": "the same forwards with the pair count read back by the host before the binning "
                                     "(gslm_forward's protocol, as the upstream forward)"},
+            "raster_streams": raster_streams,
             "num_rendered": n_rendered,
             "stage_ms": {"tangent_preprocess": tangent_ms, "render_matvec": render_ms, "gather_backward": gather_ms},
             "roofline": {"bound": "hbm", "kernel": "k_render_matvec", "achieved": achieved, "peak": HBM_PEAK_GBS,
