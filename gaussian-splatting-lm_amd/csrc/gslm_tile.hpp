@@ -68,6 +68,14 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The blend loops' exit test in two scalar ALU instructions (clang's `dmask |= stopped; if (dmask == ~0) break;`
+// was 6-8 per visit, the uniform exit lowered through a VCC select; with clear_bit, gslm_kernels.hpp).
+// live &= ~stopped, and the round's remaining hits dropped once no lane is live (s_andn2_b64 sets SCC = live != 0):
+// the loop's `while (hb)` is then its only exit test
+__device__ __forceinline__ void live_update(uint64_t& live, uint64_t& hb, uint64_t stopped) {
+  asm("s_andn2_b64 %0, %0, %2\n\ts_cselect_b64 %1, %1, 0" : "+s"(live), "+s"(hb) : "s"(stopped) : "scc");
+}
+
 // Block-wide count of `pred` over 256 threads (4 waves) with one barrier; s_cnt = 4 ints of LDS the
 // caller owns.  Replaces __syncthreads_count, whose lowering reserves 256 B of LDS per block -- the
 // difference between 3 and 4 resident blocks per CU for k_render_matvec.  Safe to call once per

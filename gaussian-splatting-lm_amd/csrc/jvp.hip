@@ -167,7 +167,7 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
     wave_lds_sync();
     while (hb) {
       const int j = (int)__builtin_ctzll(hb);
-      hb &= hb - 1ull;
+      hb = clear_bit(hb, j);
       const float4 a = s[j], b = s[64 + j], C = s[128 + j], D = s[192 + j];
       asm volatile("" : : "v"(b.z), "v"(b.w), "v"(C.x), "v"(C.y), "v"(C.z), "v"(C.w), "v"(D.x), "v"(D.y), "v"(D.z),
                    "v"(D.w));

@@ -53,9 +53,9 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
   float T = inside ? 1.0f : 0.0f;
   uint32_t last = 0;
   float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  uint64_t dmask = __builtin_amdgcn_ballot_w64(!inside);  // lanes stopped (or outside the image), wave-uniform
+  uint64_t live = __builtin_amdgcn_ballot_w64(inside);  // lanes not yet stopped (inside the image), wave-uniform
   for (int base = 0; base < n; base += 64) {
-    if (dmask == ~0ull) break;  // every pixel of this quadrant has stopped
+    if (live == 0ull) break;  // every pixel of this quadrant has stopped
     const int k = base + lane;
     bool hit = false;
     if (k < n) {
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
     wave_lds_sync();
     while (hb) {
       const int j = (int)__builtin_ctzll(hb);
-      hb &= hb - 1ull;
+      hb = clear_bit(hb, j);
       const float4 a = s[j], b = s[64 + j], cc = s[128 + j];
       asm volatile("" : : "v"(b.z), "v"(b.w), "v"(cc.x), "v"(cc.y));
       const float dx = a.x - pxf, dy = a.y - pyf;
@@ -93,8 +93,8 @@ __global__ __launch_bounds__(256) void k_render_fwd_wave(ViewK v, const uint2* _
       if (MODE == FWD_FULL) Dp = __builtin_fmaf(cc.y, wt, Dp);
       T = stop ? -fabsf(T) : test_T;
       if (MODE != FWD_LOSS) last = wt > 0.0f ? (uint32_t)(base + j + 1) : last;  // blended: 1-based list position
-      dmask |= __builtin_amdgcn_ballot_w64(stop);  // the stop compare's lane mask, no VGPR round trip
-      if (dmask == ~0ull) break;
+      // the stop compare's lane mask (no VGPR round trip) leaves `live`; the round ends when no lane is
+      live_update(live, hb, __builtin_amdgcn_ballot_w64(stop));
     }
     wave_lds_sync();
   }
@@ -155,18 +155,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
   const uint32_t* am = amask + range.x;
   float4* s = s_rec[q];
   float T[NS], C0[NS], C1[NS], C2[NS];  // T: k_render_fwd_wave's stopped-lane encoding (-|T| at the stop)
-  uint64_t dmask[NS];
-  const uint64_t out0 = __builtin_amdgcn_ballot_w64(!inside);
+  uint64_t live[NS];  // per set: lanes not yet stopped
+  const uint64_t in0 = __builtin_amdgcn_ballot_w64(inside);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
     T[a] = inside ? 1.0f : 0.0f;
     C0[a] = C1[a] = C2[a] = 0.f;
-    dmask[a] = out0;
+    live[a] = in0;
   }
   for (int base = 0; base < n; base += 64) {
     bool all = true;
 #pragma unroll
-    for (int a = 0; a < NS; ++a) all = all && dmask[a] == ~0ull;
+    for (int a = 0; a < NS; ++a) all = all && live[a] == 0ull;
     if (all) break;  // every pixel of this quadrant has stopped in every set
     const int k = base + lane;
     uint32_t g = 0u, m = 0u;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
       m = am[k] >> shift;  // sets first_set.. of the union binning (gslm_rasterize_loss_sets' first_set)
     }
     // set 0's records of this lane's entry (if it is a hit of a set still blending)
-    bool hit = dmask[0] != ~0ull && ((m >> q) & 1u);
+    bool hit = live[0] != 0ull && ((m >> q) & 1u);
     float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
     if (hit) {
       const float4* r = sr.rec[0] + RECS * (size_t)g;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
       uint64_t hb = __ballot(hit);
       wave_lds_sync();
       if (a + 1 < NS) {  // the next set's records while this set's hits are visited
-        hit = dmask[a + 1] != ~0ull && ((m >> (4 * (a + 1) + q)) & 1u);
+        hit = live[a + 1] != 0ull && ((m >> (4 * (a + 1) + q)) & 1u);
         if (hit) {
           const float4* r = sr.rec[a + 1] + RECS * (size_t)g;
           ra = r[0];
@@ -202,10 +202,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
         }
       }
       float Ta = T[a], c0 = C0[a], c1 = C1[a], c2 = C2[a];
-      uint64_t dm = dmask[a];
+      uint64_t lv = live[a];
       while (hb) {
         const int j = (int)__builtin_ctzll(hb);
-        hb &= hb - 1ull;
+        hb = clear_bit(hb, j);
         const float4 x = s[j], y = s[64 + j], z = s[128 + j];
         asm volatile("" : : "v"(y.z), "v"(y.w), "v"(z.x));
         const float dx = x.x - pxf, dy = x.y - pyf;
@@ -220,14 +220,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
         c1 = __builtin_fmaf(y.w, wt, c1);
         c2 = __builtin_fmaf(z.x, wt, c2);
         Ta = stop ? -fabsf(Ta) : test_T;
-        dm |= __builtin_amdgcn_ballot_w64(stop);
-        if (dm == ~0ull) break;
+        live_update(lv, hb, __builtin_amdgcn_ballot_w64(stop));
       }
       T[a] = Ta;
       C0[a] = c0;
       C1[a] = c1;
       C2[a] = c2;
-      dmask[a] = dm;
+      live[a] = lv;
       wave_lds_sync();  // this set's hits read before the next set's are staged
     }
   }
