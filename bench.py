@@ -34,7 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "CG matvecs/sec + raster Mpix/s, 1M Gaussians @1080p, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-RASTER_STREAMS = 4  # renders in flight for the multi-stream raster throughput (`raster_streams` in the line)
+RASTER_STREAMS = int(os.environ.get("GSLM_RASTER_STREAMS", "8"))  # renders in flight for `raster_streams` in the line
 
 
 def parse():

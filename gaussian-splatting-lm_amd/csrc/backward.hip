@@ -34,8 +34,7 @@ __global__ __launch_bounds__(256, 8) void k_render_bwd(ViewK v, const uint2* __r
   // whose partials at 128 entries took 24-26 KB of LDS per block -> 6 blocks per CU, at 96 entries 17.9-19.5 KB -> 8
   // blocks per CU, and under __launch_bounds__(256, 8) 44-45 VGPRs (74-76 without the hint): 8 waves per SIMD
   constexpr int B = WITH_XY ? 96 : 128;
-  __shared__ float4 s_r0[B], s_r1[B];
-  __shared__ float2 s_r2[B];
+  __shared__ float2 s_rp[5 * B];  // vjp_tile's record planes
   __shared__ uint64_t s_bits[16];
   __shared__ float s_acc[vjp_acc_floats<WITH_XY, WITH_INV, B>()];
   __shared__ int s_misc[4];
@@ -60,7 +59,7 @@ __global__ __launch_bounds__(256, 8) void k_render_bwd(ViewK v, const uint2* __r
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, d0, d1, d2, di);
   vjp_tile<WITH_XY, WITH_INV, ROWF4, B>(st, inside, (float)px, (float)py, tile_x, tile_y, ranges[tile], point_list,
-                                     rec, slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, rows,
+                                     rec, slots, rect, goff, s_rp, s_bits, s_acc, s_misc, rows,
                                      write_tail != 0);
 }
 

@@ -246,7 +246,6 @@ __device__ __forceinline__ uint64_t wave_bits(const uint64_t* s_bits, int s, int
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Wave-uniform iterator over wave s's hit set of the current batch, in list order.
 // Mask m with bit j cleared, one scalar ALU instruction: the hit loops' `hb &= hb - 1` for j = ctz(hb) was three
 // (s_add_u32 + s_addc_u32 + s_and_b64), and those loops issue about as many SALU as VALU instructions per visit.
 // Register-only (no memory access).
@@ -255,6 +254,7 @@ __device__ __forceinline__ uint64_t clear_bit(uint64_t m, int j) {
   return m;
 }
 
+// Wave-uniform iterator over wave s's hit set of the current batch, in list order.
 struct HitIter {
   const uint64_t* s_bits;
   uint64_t cur;

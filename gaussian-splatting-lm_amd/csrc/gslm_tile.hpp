@@ -181,13 +181,16 @@ constexpr int vjp_acc_floats() { return 4 * n_used<WITH_XY, WITH_INV>() * acc_st
 // reduced row per (tile, Gaussian) pair.  Block-uniform control flow; requires blockDim = 256.
 // slots != NULL (the LM row map): rows exist for head entries only -- those some wave still blending at their list
 // position visits (a non-empty mask below) -- and the others are not written.
+// s_rp: the batch's records as five float2 planes of BATCH entries ((x, y), (conic a, b), (conic c, opacity), (r, g),
+// (b, 1/depth)): a visit reads entry j of each plane from ONE address (8 j) with plane offsets -- two
+// ds_read2st64_b64 and a ds_read_b64, issued together -- where the float4 / float2 arrays needed two addresses of
+// different scale and the float2 read waited behind the float4 pair.
 template <bool WITH_XY, bool WITH_INV, int ROWF4, int BATCH>
 __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, float pyf, int tile_x, int tile_y,
                                          uint2 range, const uint32_t* __restrict__ point_list,
                                          const float4* __restrict__ rec, const uint32_t* __restrict__ slots,
                                          const uint2* __restrict__ rect, const uint32_t* __restrict__ goff,
-                                         float4* s_r0, float4* s_r1,
-                                         float2* s_r2, uint64_t* s_bits, float* s_acc, int* s_misc,
+                                         float2* s_rp, uint64_t* s_bits, float* s_acc, int* s_misc,
                                          float4* __restrict__ rows, bool write_tail) {
   constexpr int NU = n_used<WITH_XY, WITH_INV>();
   constexpr int ACC_STRIDE = acc_stride<BATCH>();
@@ -227,10 +230,12 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
       const uint32_t e = point_list[range.x + base - tid];
       const uint32_t g = pl_id(e);
       my_mask = pl_mask(e);
-      s_r0[tid] = rec[RECS * (int64_t)g + 0];
-      s_r1[tid] = rec[RECS * (int64_t)g + 1];
-      const float4 r2 = rec[RECS * (int64_t)g + 2];
-      s_r2[tid] = make_float2(r2.x, r2.y);
+      const float4 r0 = rec[RECS * (int64_t)g + 0], r1 = rec[RECS * (int64_t)g + 1], r2 = rec[RECS * (int64_t)g + 2];
+      s_rp[tid] = make_float2(r0.x, r0.y);
+      s_rp[BATCH + tid] = make_float2(r0.z, r0.w);
+      s_rp[2 * BATCH + tid] = make_float2(r1.x, r1.y);
+      s_rp[3 * BATCH + tid] = make_float2(r1.z, r1.w);
+      s_rp[4 * BATCH + tid] = make_float2(r2.x, r2.y);
       // and only the waves that still blend at this list position
       const int pos = base - tid;
       my_mask &= (pos < wm0 ? 1u : 0u) | (pos < wm1 ? 2u : 0u) | (pos < wm2 ? 4u : 0u) | (pos < wm3 ? 8u : 0u);
@@ -242,10 +247,18 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
     // takes zero for the others (exactly what a visit with no valid lane would have produced)
     publish_quad_masks(my_mask, s_bits);
     __syncthreads();
-    HitIter it(s_bits, w);
-    for (int j = it.next(); j >= 0; j = it.next()) {
-      const float4 a = s_r0[j], b = s_r1[j];
-      const float2 c = s_r2[j];
+    // the batch's hit words in order, each walked by s_ff1 (HitIter's single loop cost ~5 more scalar instructions per
+    // visit: the word switch, a sign test of the index and a branch through the iterator's exit)
+#pragma unroll 1
+    for (int wd = 0; wd < (BATCH + 63) / 64; ++wd) {
+    uint64_t hits = wave_bits(s_bits, w, wd);
+    while (hits) {
+      const int hb = (int)__builtin_ctzll(hits);
+      hits = clear_bit(hits, hb);
+      const int j = 64 * wd + hb;
+      const float2 p0 = s_rp[j], p1 = s_rp[BATCH + j], p2 = s_rp[2 * BATCH + j], p3 = s_rp[3 * BATCH + j];
+      const float2 c = s_rp[4 * BATCH + j];
+      const float4 a = make_float4(p0.x, p0.y, p1.x, p1.y), b = make_float4(p2.x, p2.y, p3.x, p3.y);
       // the whole record in one LDS round trip at the top of the iteration (the empty asm pins the loads
       // here; otherwise the colour half is fetched after the alpha test, a second exposed LDS latency;
       // prefetching the next hit's record instead measured 9% slower: it costs issue slots, not latency)
@@ -349,6 +362,7 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         }
       }
     }
+    }
     __syncthreads();
     // rows only for the entries some wave visited: the LM rows (slots) exist for head entries only (k_row_flags); the
     // drop-in's rectangle rows of every other entry are the zeros its caller filled the buffer with (write_tail = 0),
@@ -372,13 +386,13 @@ __device__ __forceinline__ void vjp_tile(VjpPix& st, bool inside, float pxf, flo
         }
       }
       // the conic rows' factors o (-1/2, -1, -1/2) (see the hit loop)
-      const float op = s_r1[tid].y;
+      const float op = s_rp[2 * BATCH + tid].y;
       t[2] *= -0.5f * op;
       t[3] *= -op;
       t[4] *= -0.5f * op;
       if (WITH_XY) {  // o sum gv5 dx, o sum gv5 dy -> dL/d(x, y) with the entry's conic (A, B, C)
 #pragma clang fp contract(fast)
-        const float cA = s_r0[tid].z, cB = s_r0[tid].w, cC = s_r1[tid].x, sx = op * t[0], sy = op * t[1];
+        const float cA = s_rp[BATCH + tid].x, cB = s_rp[BATCH + tid].y, cC = s_rp[2 * BATCH + tid].x, sx = op * t[0], sy = op * t[1];
         t[0] = -(cA * sx + cB * sy);
         t[1] = -(cC * sy + cB * sx);
       }

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256, WITH_XY ? 6 : 8) void k_render_matvec(ViewK v,
                                                         const uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ weight, float4* __restrict__ contrib,
                                                         int write_tail) {
-  // 128-entry batches.  The LM instantiation (WITH_XY = false): 19.7 KB of LDS and 56 VGPRs -> 8 blocks per CU, 8
+  // 128-entry batches.  The LM instantiation (WITH_XY = false): 20.1 KB of LDS and 47 VGPRs -> 8 blocks per CU, 8
   // waves per SIMD (hipcc -Rpass-analysis=kernel-resource-usage; profiles/r04/resource_usage.txt); the drop-in
   // one (screen-position tangents): 23.8 KB, 64 VGPRs -> 6 blocks per CU
   constexpr int B = MATVEC_BATCH;
@@ -277,8 +277,9 @@ __global__ __launch_bounds__(256, WITH_XY ? 6 : 8) void k_render_matvec(ViewK v,
   // live together (vjp_tile starts with a block barrier): one LDS region.  Without screen-position tangents
   // the JVP pass runs one independent wave per quadrant (jvp_wave_packed: 4 x 256 float4 of wave-private
   // records); with them the block-cooperative jvp_tile.
-  constexpr int kAcc = (vjp_acc_floats<WITH_XY, false, B>() + 3) / 4;  // float4
-  constexpr int kVjp = kAcc + B + B + B / 2;                             // + s_r0, s_r1, s_r2
+  // float4; rounded up to 512 B: vjp_tile's record planes then start on a ds_read2st64 stride (no address add per visit)
+  constexpr int kAcc = (vjp_acc_floats<WITH_XY, false, B>() + 3) / 4 + 31 & ~31;
+  constexpr int kVjp = kAcc + B + B + B / 2;  // + s_r0, s_r1, s_r2 (vjp_tile: 5 float2 planes)
   constexpr int kJvp = WITH_XY ? 0 : 4 * 256;
   static_assert(!WITH_XY || kAcc >= 2 * B + B / 2, "jvp_tile's tangent records must fit below s_r0");
   __shared__ float4 s_lds[kVjp > kJvp ? kVjp : kJvp];
@@ -326,7 +327,8 @@ __global__ __launch_bounds__(256, WITH_XY ? 6 : 8) void k_render_matvec(ViewK v,
   VjpPix st;
   vjp_init(st, v, inside, Tf, last, u0, u1, u2, 0.f);
   vjp_tile<WITH_XY, false, WITH_XY ? 3 : 2, B>(st, inside, (float)px, (float)py, tile_x, tile_y, range, point_list, rec,
-                                            slots, rect, goff, s_r0, s_r1, s_r2, s_bits, s_acc, s_misc, contrib, write_tail != 0);
+                                            slots, rect, goff, reinterpret_cast<float2*>(s_r0), s_bits, s_acc, s_misc, contrib,
+                                            write_tail != 0);
 }
 
 // ------------------------------------------------------------------ launchers
