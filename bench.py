@@ -302,38 +302,6 @@ def main():
     barrier()
     t_fwd_sync = max_over_ranks(time.perf_counter() - t0)  # (leaves every view in forward()'s exact layout)
     mpix_sync = n_views * W * H * fsteps / t_fwd_sync / 1e6
-    # the same device-count forwards with RASTER_STREAMS renders in flight on as many HIP streams (the line search's
-    # setting: independent validation renders overlap, a render's launch-bound sort passes beside another's blend) --
-    # a throughput over many renders, reported beside the one-stream rate above, which stays `raster_mpix_s`
-    raster_streams = None
-    if not args.no_side and prob.views:
-        from gslm.lm import ViewRaster
-        S = RASTER_STREAMS
-        vr0 = prob.views[0]
-        rasters = [ViewRaster(vr0.view, device) for _ in range(S)]
-        streams = [torch.cuda.Stream(device) for _ in range(S)]
-        for r, st in zip(rasters, streams):
-            r.forward(graw, st.cuda_stream)
-        capz = [r.capacity() for r in rasters]
-        cnt_s = torch.zeros(max(fsteps, 1) * S, dtype=torch.int32, device=device)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for it in range(fsteps):
-            for j, (r, st) in enumerate(zip(rasters, streams)):
-                r.forward_dev(graw, st.cuda_stream, n_out=cnt_s.data_ptr() + 4 * (it * S + j))
-        torch.cuda.synchronize()
-        t_s = time.perf_counter() - t0
-        cs = cnt_s.view(max(fsteps, 1), S).tolist()
-        if any(c[j] > capz[j] for c in cs[:fsteps] for j in range(S)):
-            raise RuntimeError("raster_streams: a pair count exceeded its list capacity")
-        raster_streams = {"streams": S, "renders": S * fsteps, "mpix_s": S * fsteps * W * H / t_s / 1e6,
-                          "ms_per_render": 1e3 * t_s / (S * fsteps),
-                          "note": f"{S} independent forwards of view 0 in flight on {S} HIP streams (gslm_rasterize_dev, "
-                                  "counts checked after the loop): render throughput, not one forward's latency "
-                                  "(raster_mpix_s / forward_ms_per_view)"}
-        del rasters, streams
-        torch.cuda.empty_cache()
-
     # ---------------- roofline of the dominant kernel: the fused JVP->VJP tile pass (k_render_matvec)
     loc = getattr(prob, "local", prob)  # the rank's own LMProblem (full P) under a sharded operator
     vr = loc.views[0]
@@ -420,8 +388,43 @@ def main():
     n_views_local = len(loc.views)
     sh_proj = prob.layout.rest_projected
     exchange = prob.exchange if (world_size > 1 or forced) else "none"
+    view0 = prob.views[0].view if prob.views else None
     del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
+
+    # the raster forwards with RASTER_STREAMS renders in flight on as many HIP streams (the line search's setting:
+    # independent validation renders overlap, a render's launch-bound sort passes beside another's blend) -- a
+    # throughput over many renders, reported beside the one-stream rate, which stays `raster_mpix_s`.  Run after the
+    # roofline's kernel timing (which it would otherwise precede: the stage timing right after this burst of 8-stream
+    # work measured k_render_matvec 7% slower than rocprof's solo average) and with the problem's memory released
+    raster_streams = None
+    if not args.no_side and view0 is not None:
+        from gslm.lm import ViewRaster
+        S = RASTER_STREAMS
+        rasters = [ViewRaster(view0, device) for _ in range(S)]
+        streams = [torch.cuda.Stream(device) for _ in range(S)]
+        for r, st in zip(rasters, streams):
+            r.forward(graw, st.cuda_stream)
+        capz = [r.capacity() for r in rasters]
+        cnt_s = torch.zeros(max(fsteps, 1) * S, dtype=torch.int32, device=device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(fsteps):
+            for j, (r, st) in enumerate(zip(rasters, streams)):
+                r.forward_dev(graw, st.cuda_stream, n_out=cnt_s.data_ptr() + 4 * (it * S + j))
+        torch.cuda.synchronize()
+        t_s = time.perf_counter() - t0
+        cs = cnt_s.view(max(fsteps, 1), S).tolist()
+        if any(c[j] > capz[j] for c in cs[:fsteps] for j in range(S)):
+            raise RuntimeError("raster_streams: a pair count exceeded its list capacity")
+        raster_streams = {"streams": S, "renders": S * fsteps, "mpix_s": S * fsteps * W * H / t_s / 1e6,
+                          "ms_per_render": 1e3 * t_s / (S * fsteps),
+                          "note": f"{S} independent forwards of view 0 in flight on {S} HIP streams (gslm_rasterize_dev, "
+                                  "counts checked after the loop): render throughput, not one forward's latency "
+                                  "(raster_mpix_s / forward_ms_per_view)"}
+        del rasters, streams
+        torch.cuda.empty_cache()
+
 
     fb = c0_gpu = lm = lm_tv = lm_ref = ssim = fo = dropin = None
     if not args.no_side:
