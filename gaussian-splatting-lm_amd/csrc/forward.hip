@@ -336,16 +336,22 @@ __global__ __launch_bounds__(1024) void k_tile_order(int ntiles, const uint2* __
   };
   for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
   __syncthreads();
-  // exclusive scan of the 1024 bucket counts (Hillis-Steele on an inclusive copy)
-  uint32_t v = s_cnt[tid];
-  for (int o = 1; o < 1024; o <<= 1) {
-    __syncthreads();
-    const uint32_t a = tid >= o ? s_cnt[tid - o] : 0u;
-    __syncthreads();
-    s_cnt[tid] += a;
+  // exclusive scan of the 1024 bucket counts: each wave's 64 by shuffles, then the 16 wave totals (two barriers;
+  // a block-wide Hillis-Steele scan took 20)
+  __shared__ uint32_t s_wsum[16];
+  const int lane = tid & 63, w = tid >> 6;
+  const uint32_t v = s_cnt[tid];
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
+  if (lane == 63) s_wsum[w] = inc;
   __syncthreads();
-  s_cnt[tid] -= v;  // exclusive
+  uint32_t wbase = 0u;
+  for (int k = 0; k < w; ++k) wbase += s_wsum[k];
+  s_cnt[tid] = wbase + inc - v;  // exclusive
   __syncthreads();
   for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
 }
@@ -356,20 +362,39 @@ __global__ __launch_bounds__(256) void k_point_ids(int64_t N, const uint32_t* __
   if (k < N) out[k] = pl_id(pl[k]);
 }
 
-// n_dev (or NULL): as k_duplicate (N the capacity, *n_dev the count); n_out (or NULL) receives the count
+// n_dev (or NULL): as k_duplicate (N the capacity, *n_dev the count); n_out (or NULL) receives the count.
+// RANGES_KEYS consecutive keys per thread from one 16-B load (the list's key buffers are 256-B aligned), the keys just
+// before and after the group from memory (the neighbouring threads' loads: cache hits): a quarter of the threads of a
+// key per thread, each with one vector load instead of three scalar ones.
+constexpr int RANGES_KEYS = 4;
 __global__ __launch_bounds__(256) void k_ranges(int64_t N, const uint32_t* __restrict__ keys,
                                                  uint2* __restrict__ ranges, const uint32_t* __restrict__ n_dev,
                                                  uint32_t* __restrict__ n_out) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k0 = RANGES_KEYS * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (n_dev) {
     const uint32_t c = *n_dev;
-    if (n_out && k == 0) *n_out = c;
+    if (n_out && k0 == 0) *n_out = c;
     N = min(N, (int64_t)c);
   }
-  if (k >= N) return;
-  const uint32_t t = keys[k];
-  if (k == 0 || keys[k - 1] != t) ranges[t].x = (uint32_t)k;
-  if (k == N - 1 || keys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
+  if (k0 >= N) return;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;  // never a tile id: a list edge
+  uint32_t t[RANGES_KEYS];
+  if (k0 + RANGES_KEYS <= N) {
+    const uint4 v = *reinterpret_cast<const uint4*>(keys + k0);
+    t[0] = v.x, t[1] = v.y, t[2] = v.z, t[3] = v.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < RANGES_KEYS; ++j) t[j] = k0 + j < N ? keys[k0 + j] : NONE;
+  }
+  const uint32_t before = k0 > 0 ? keys[k0 - 1] : NONE;
+  const uint32_t after = k0 + RANGES_KEYS < N ? keys[k0 + RANGES_KEYS] : NONE;
+#pragma unroll
+  for (int j = 0; j < RANGES_KEYS; ++j) {
+    if (t[j] == NONE) break;  // past the list's end
+    const uint32_t p = j ? t[j - 1] : before, q = j + 1 < RANGES_KEYS ? t[j + 1] : after;
+    if (p != t[j]) ranges[t[j]].x = (uint32_t)(k0 + j);
+    if (q != t[j]) ranges[t[j]].y = (uint32_t)(k0 + j + 1);
+  }
 }
 
 // ---- the LM row map (ScratchBufs::hscan), once per geometry ----
@@ -679,7 +704,7 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
       set_error("internal: radix pass count disagrees with the union binning layout");
       return GSLM_ERR_INVALID;
     }
-    const unsigned nbN = (unsigned)((N + 255) / 256);
+    const unsigned nbN = (unsigned)((N + 256 * RANGES_KEYS - 1) / (256 * RANGES_KEYS));
     hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, (const uint32_t*)nullptr,
                        (uint32_t*)nullptr);
     GSLM_LAUNCH_CHECK();
@@ -756,7 +781,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
     set_error("internal: radix pass count disagrees with the binning layout");
     return GSLM_ERR_INVALID;
   }
-  const unsigned nbN = (unsigned)((N + 255) / 256);
+  const unsigned nbN = (unsigned)((N + 256 * RANGES_KEYS - 1) / (256 * RANGES_KEYS));
   hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, n_dev, n_out);
   GSLM_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
