@@ -264,15 +264,24 @@ int launch_preprocess_views(const PreViewsK& pv, const GaussK& g, const GeomBufs
 // n_dev (or NULL): N is the list capacity and *n_dev the pair count (the depth-order scan's total, not read back
 // by the host: gslm_rasterize_dev); pairs past the capacity are not written (the host sees the count and renders
 // that view again with a larger list)
+// zero_ranges (ntiles of them): the tile ranges the binning's k_ranges fills afterwards, zeroed here by a grid-stride
+// store (every range left [0, 0) stays an empty tile) -- one memset launch less per binning
+__device__ __forceinline__ void zero_tile_ranges(uint2* __restrict__ ranges, int ntiles) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x)
+    ranges[t] = make_uint2(0u, 0u);
+}
+
 __global__ __launch_bounds__(256) void k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ sorted_idx,
                                                     const uint32_t* __restrict__ offsets, uint32_t N,
                                                     const uint32_t* __restrict__ n_dev,
                                                     const uint2* __restrict__ rect, const float4* __restrict__ rec,
-                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    uint2* __restrict__ zero_ranges, int ntiles) {
   __shared__ QuadCull s_q[256];
   __shared__ uint32_t s_off[257];
   __shared__ uint32_t s_g[256];
   __shared__ uint32_t s_rc[256][3];  // x0, y0, width
+  zero_tile_ranges(zero_ranges, ntiles);
   const int tid = threadIdx.x;
   const int64_t s0 = (int64_t)blockIdx.x * 256, s = s0 + tid;
   const int64_t slast = min(s0 + 255, P - 1);
@@ -578,8 +587,10 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_duplicate_union(int64_t P, int gx, const uint32_t* __restrict__ offsets,
                                                           uint32_t N, const uint2* __restrict__ urect, UnionSets u,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                          uint32_t* __restrict__ amask) {
+                                                          uint32_t* __restrict__ amask, uint2* __restrict__ zero_ranges,
+                                                          int ntiles) {
   extern __shared__ float4 s_set[];  // [NS][2][DUPU_G]
+  zero_tile_ranges(zero_ranges, ntiles);
   __shared__ uint2 s_srect[NS][DUPU_G];
   __shared__ float2 s_gxy[DUPU_G];
   __shared__ uint32_t s_off[DUPU_G + 1];
@@ -678,15 +689,15 @@ int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStre
 int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,
                          int64_t N, const UnionSets& u, hipStream_t s) {
   const int ntiles = v.gx * v.gy;
-  GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
-  if (P > 0 && N > 0) {
+  if (P == 0 || N == 0) GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
+  if (P > 0 && N > 0) {  // (k_duplicate_union also zeroes the tile ranges)
     const size_t lds = (size_t)u.n * 2 * DUPU_G * sizeof(float4);
     const dim3 grid((unsigned)((P + DUPU_G - 1) / DUPU_G));
     switch (u.n) {
 #define GSLM_DUP_UNION(NS)                                                                                         \
   case NS:                                                                                                         \
     hipLaunchKernelGGL(k_duplicate_union<NS>, grid, dim3(256), lds, s, P, v.gx, ug.offsets, (uint32_t)N, ug.rect, u, \
-                       bb.keys0, bb.vals0, um.m0);                                                                   \
+                       bb.keys0, bb.vals0, um.m0, bb.ranges, ntiles);                                                \
     break;
       GSLM_DUP_UNION(1) GSLM_DUP_UNION(2) GSLM_DUP_UNION(3) GSLM_DUP_UNION(4)
       GSLM_DUP_UNION(5) GSLM_DUP_UNION(6) GSLM_DUP_UNION(7) GSLM_DUP_UNION(8)
@@ -759,10 +770,11 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   const int ntiles = v.gx * v.gy;
   // device_count: N is the list capacity, the pair count stays on the device (gb.counters[0])
   const uint32_t* n_dev = device_count ? gb.counters : nullptr;
-  GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
-  if (P > 0)
+  if (P > 0)  // (k_duplicate also zeroes the tile ranges)
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, v.gx, gb.sorted_idx,
-                       gb.offsets, (uint32_t)N, n_dev, gb.rect, gb.rec, bb.keys0, bb.vals0);
+                       gb.offsets, (uint32_t)N, n_dev, gb.rect, gb.rec, bb.keys0, bb.vals0, bb.ranges, ntiles);
+  else
+    GSLM_HIP_CHECK(hipMemsetAsync(bb.ranges, 0, (size_t)ntiles * sizeof(uint2), s));
   GSLM_LAUNCH_CHECK();
   if (N == 0) {  // every range stays [0, 0); the tile passes still read a launch order
     if (n_out) {

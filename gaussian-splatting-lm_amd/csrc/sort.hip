@@ -49,6 +49,17 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
   return inc + off;
 }
 
+// The exclusive prefix of the first b of a scan's per-block sums (written raw by the reduce pass), summed by the
+// block's threads (b <= a few thousand: L2-resident loads).  In the apply pass this replaces the scan-of-block-sums
+// launch between the two passes (a single-block kernel at its ~5 us floor, twice per forward).
+__device__ __forceinline__ uint32_t block_sums_before(const uint32_t* __restrict__ bs, int b, uint32_t* s_w) {
+  uint32_t acc = 0;
+  for (int i = threadIdx.x; i < b; i += blockDim.x) acc += bs[i];
+  uint32_t tot;
+  block_incl_scan256(acc, s_w, &tot);
+  return tot;
+}
+
 // n_dev (or NULL): the key count is min(n, *n_dev), read on the device (a capacity-sized launch whose count the host
 // has not read back: gslm_rasterize_dev); blocks past it count nothing
 template <int ITEMS>
@@ -216,29 +227,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* __
   if (tid == 0) block_sums[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ block_sums, int nb,
-                                                  uint32_t* __restrict__ total) {
-  __shared__ uint32_t s_w[4];
-  const int tid = threadIdx.x;
-  uint32_t carry = 0;
-  for (int base = 0; base < nb; base += 256) {
-    const int i = base + tid;
-    const uint32_t x = i < nb ? block_sums[i] : 0u;
-    uint32_t tot;
-    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
-    if (i < nb) block_sums[i] = carry + inc - x;
-    carry += tot;
-  }
-  if (tid == 0) *total = carry;
-}
-
 // In-place form of k_scan_apply (data = in = out, no index gather): one pointer without __restrict__, so the
 // compiler keeps every thread's loads of its elements ahead of its stores to them.
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* data, int64_t n,
-                                                                     const uint32_t* __restrict__ block_sums) {
+                                                                     const uint32_t* __restrict__ block_sums,
+                                                                     uint32_t* __restrict__ total) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  const uint32_t before = block_sums_before(block_sums, blockIdx.x, s_w);
   uint32_t v[SCAN_ITEMS];
   uint32_t acc = 0;
 #pragma unroll
@@ -249,7 +246,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* d
   }
   uint32_t tot;
   const uint32_t inc = block_incl_scan256(acc, s_w, &tot);
-  uint32_t run = block_sums[blockIdx.x] + inc - acc;
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) *total = before + tot;
+  uint32_t run = before + inc - acc;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const int64_t i = base + k;
@@ -261,10 +259,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* d
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __restrict__ in,
                                                              const uint32_t* __restrict__ idx, int64_t n,
                                                              const uint32_t* __restrict__ block_sums,
-                                                             uint32_t* __restrict__ out) {
+                                                             uint32_t* __restrict__ out, uint32_t* __restrict__ total) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  const uint32_t before = block_sums_before(block_sums, blockIdx.x, s_w);
   uint32_t v[SCAN_ITEMS];
   uint32_t acc = 0;
 #pragma unroll
@@ -275,7 +274,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __r
   }
   uint32_t tot;
   const uint32_t inc = block_incl_scan256(acc, s_w, &tot);
-  uint32_t run = block_sums[blockIdx.x] + inc - acc;
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) *total = before + tot;
+  uint32_t run = before + inc - acc;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const int64_t i = base + k;
@@ -312,32 +312,18 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_reduce(const uint32_t* _
   }
 }
 
-// blockIdx.x = 0 scans the a partials, 1 the b partials
-__global__ __launch_bounds__(256) void k_scan2_top(uint32_t* __restrict__ block_sums, int nb,
-                                                   uint32_t* __restrict__ total_a, uint32_t* __restrict__ total_b) {
-  __shared__ uint32_t s_w[4];
-  const int tid = threadIdx.x;
-  uint32_t* bs = block_sums + (int64_t)blockIdx.x * nb;
-  uint32_t carry = 0;
-  for (int base = 0; base < nb; base += 256) {
-    const int i = base + tid;
-    const uint32_t x = i < nb ? bs[i] : 0u;
-    uint32_t tot;
-    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
-    if (i < nb) bs[i] = carry + inc - x;
-    carry += tot;
-  }
-  if (tid == 0) *(blockIdx.x == 0 ? total_a : total_b) = carry;
-}
-
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __restrict__ in,
                                                               const uint32_t* __restrict__ idx,
                                                               const uint32_t* __restrict__ in_b, int64_t n,
                                                               const uint32_t* __restrict__ block_sums,
-                                                              uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b) {
+                                                              uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b,
+                                                              uint32_t* __restrict__ total_a,
+                                                              uint32_t* __restrict__ total_b) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+  const uint32_t before_a = block_sums_before(block_sums, blockIdx.x, s_w);
+  const uint32_t before_b = block_sums_before(block_sums + gridDim.x, blockIdx.x, s_w);
   uint32_t va[SCAN_ITEMS], vb[SCAN_ITEMS];
   uint32_t acc_a = 0, acc_b = 0;
 #pragma unroll
@@ -348,11 +334,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __
     acc_a += va[k];
     acc_b += vb[k];
   }
-  uint32_t tot;
-  const uint32_t inc_a = block_incl_scan256(acc_a, s_w, &tot);
-  const uint32_t inc_b = block_incl_scan256(acc_b, s_w, &tot);
-  uint32_t ra = block_sums[blockIdx.x] + inc_a - acc_a;
-  uint32_t rb = block_sums[gridDim.x + blockIdx.x] + inc_b - acc_b;
+  uint32_t tot_a, tot_b;
+  const uint32_t inc_a = block_incl_scan256(acc_a, s_w, &tot_a);
+  const uint32_t inc_b = block_incl_scan256(acc_b, s_w, &tot_b);
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) {
+    *total_a = before_a + tot_a;
+    *total_b = before_b + tot_b;
+  }
+  uint32_t ra = before_a + inc_a - acc_a;
+  uint32_t rb = before_b + inc_b - acc_b;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const int64_t i = base + k;
@@ -376,8 +366,8 @@ int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* o
   }
   const int nb = (int)scan_blocks(n);
   hipLaunchKernelGGL(k_scan2_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp);
-  hipLaunchKernelGGL(k_scan2_top, dim3(2), dim3(256), 0, s, tmp, nb, total_a, total_b);
-  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b);
+  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b, total_a,
+                     total_b);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -438,11 +428,10 @@ int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, i
   }
   const int nb = (int)scan_blocks(n);
   hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, tmp, nb, total);
   if (out == in && !idx)  // in place (the LM row map's head-flag scan)
-    hipLaunchKernelGGL(k_scan_apply_inplace, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp);
+    hipLaunchKernelGGL(k_scan_apply_inplace, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp, total);
   else
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out, total);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
