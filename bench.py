@@ -531,6 +531,8 @@ def main():
         json_out.flush()
     if dist.is_initialized():
         dist.barrier()
+        from gslm.parallel import close_native_comms
+        close_native_comms()  # (GSLM_COMM=native) every rank at the same point, before the process group goes
         dist.destroy_process_group()
 
 

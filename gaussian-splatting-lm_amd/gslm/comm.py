@@ -13,6 +13,7 @@ after it (Work.wait()).
 """
 import ctypes
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -64,6 +65,11 @@ class NativeComm:
             self.handle = None
 
     def __del__(self):
+        # never at interpreter teardown: ranks reach it in no set order and the HIP runtime may already be gone, so a
+        # communicator the program did not close() is left to process exit (the driver frees its resources); an
+        # orderly shutdown calls close() on every rank before destroying the process group
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

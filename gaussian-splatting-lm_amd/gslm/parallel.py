@@ -57,6 +57,16 @@ def native_comm(group=None, device=None):
     return _NATIVE[key]
 
 
+def close_native_comms():
+    """Destroy the GSLM_COMM=native communicators, in creation order, after the device's work: call it on every rank
+    at the same point of an orderly shutdown (before destroy_process_group) -- NativeComm.__del__ does not run at
+    interpreter teardown."""
+    if _NATIVE:
+        torch.cuda.synchronize()
+    for key in list(_NATIVE):
+        _NATIVE.pop(key).close()
+
+
 def _device_allreduce(t, group):
     """In-place sum over the ranks: the native communicator for device tensors under GSLM_COMM=native, otherwise
     torch.distributed (host-staged under gloo)."""

@@ -109,6 +109,8 @@ def main():
         "step_rel": float(np.linalg.norm(r["step"].cpu().numpy() - s_ref) / np.linalg.norm(s_ref)),
         "final_rel": abs(r["final_val_loss"] - float(L["ten_final_val_loss"])) / float(L["ten_final_val_loss"])}
     dist.barrier()
+    from gslm.parallel import close_native_comms
+    close_native_comms()  # the exchanges' cached GSLM_COMM=native communicator, before the process group
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)
 
