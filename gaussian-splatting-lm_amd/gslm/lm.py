@@ -815,11 +815,14 @@ class LossEvaluator:
         array read once at the end, and a view whose count exceeded its slot's list capacity is rendered again
         exactly (its slot grown).
       * Streams: consecutive views of a batch run on `streams` HIP streams, so one view's short serial kernels
-        (scans, the tile launch order, the loss reduction) and its blend's tail overlap another view's work.
+        (scans, the tile launch order, the loss reduction) and its blend's tail overlap another view's work.  Three
+        by default: with the main stream that is the 4 hardware queues HIP gives a process (GPU_MAX_HW_QUEUES), and
+        the LM step measured 91-93 ms at 3 side streams against 94-96 at 8 (profiles/r05/ab/val_streams_kept/; more
+        queues or higher-priority streams were slower still).
     Each view's loss lands in its own device double; the total is their sum (view order fixed, so run to run the
     same).  `reduce`: a callable summing it over the ranks that hold the other views (gslm.parallel.allreduce_loss)."""
 
-    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None, streams=8,
+    def __init__(self, model, cams, bg, device="cuda", batch=8, gts=None, alpha_masks=None, reduce=None, streams=3,
                  device_count=False):
         self.model = model
         # True: evaluations after the first render through gslm_rasterize_loss_dev (no count read-back per batch).
@@ -1281,7 +1284,9 @@ def lm_step(model, cams, val_cams, bg, max_iter=2, restart_iter=1, damp=None, ma
     else:
         _VAL_CACHE.pop("last", None)
         val = evaluator_cls(model, mine_val, bg, device=device, batch=val_batch,
-                            reduce=(lambda x: allreduce_loss(x, group)) if sharded else None)
+                            reduce=(lambda x: allreduce_loss(x, group)) if sharded else None,
+                            # (GSLM_VAL_STREAMS: the side-stream count, an A/B override of LossEvaluator's default)
+                            **({"streams": int(os.environ["GSLM_VAL_STREAMS"])} if "GSLM_VAL_STREAMS" in os.environ else {}))
         if cache_val:
             val.held = (model, list(mine_val), imgs)
             _VAL_CACHE["last"] = (vkey, val)
