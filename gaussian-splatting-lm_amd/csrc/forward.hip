@@ -365,6 +365,118 @@ __global__ __launch_bounds__(1024) void k_tile_order(int ntiles, const uint2* __
   for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
 }
 
+// XCD-aware form of the launch order (the LM product's).  Blocks are dealt round-robin over the 8
+// XCDs, so blocks b and b + 8 share one XCD's L2 (MI355X_MICROARCH.md §Workgroup dispatch: observed, a speed choice,
+// never correctness).  The tiles are cut, in row-major order, into XG contiguous bands of equal total weight (the
+// cost key, or the list length, + 1), band g longest-first as k_tile_order orders the whole frame, and band g's k-th
+// tile launched as block 8 k + g while every band still has tiles (the bands' leftover, cheapest tiles close the
+// order).  Each XCD then gathers the records of about an eighth of the frame's Gaussians instead of all of them.
+constexpr int XG = 8;
+__global__ __launch_bounds__(1024) void k_tile_order_xcd(int ntiles, const uint2* __restrict__ ranges,
+                                                          uint32_t* __restrict__ order,
+                                                          const uint32_t* __restrict__ cost) {
+  __shared__ uint32_t s_cnt[XG][1024];
+  __shared__ unsigned long long s_w64[16];
+  __shared__ uint32_t s_w32[16];
+  __shared__ uint32_t s_n[XG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto len = [&](int t) { return cost ? cost[t] : ranges[t].y - ranges[t].x; };
+  auto bucket = [&](uint32_t n) { return 1023u - (n < 768u ? n : min(1023u, 768u + ((n - 768u) >> 5))); };
+  // 1. each thread a contiguous run of tiles: its weight, the block-wide exclusive prefix of the runs' weights
+  const int seg = (ntiles + 1023) / 1024, t0 = min(ntiles, tid * seg), t1 = min(ntiles, t0 + seg);
+  unsigned long long mine = 0ull;
+  for (int t = t0; t < t1; ++t) mine += (unsigned long long)len(t) + 1ull;
+  unsigned long long inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_w64[w] = inc;
+#pragma unroll
+  for (int g = 0; g < XG; ++g) s_cnt[g][tid] = 0u;
+  __syncthreads();
+  unsigned long long before = 0ull, total = 0ull;
+  for (int k = 0; k < 16; ++k) {
+    if (k < w) before += s_w64[k];
+    total += s_w64[k];
+  }
+  before += inc - mine;
+  // band of a tile: where the middle of its weight falls in the frame's total
+  auto band = [&](unsigned long long pre, uint32_t wt) {
+    return (int)min((unsigned long long)(XG - 1), ((2ull * pre + wt) * XG) / (2ull * total));
+  };
+  // 2. histogram of (band, length bucket)
+  {
+    unsigned long long pre = before;
+    for (int t = t0; t < t1; ++t) {
+      const uint32_t n = len(t);
+      atomicAdd(&s_cnt[band(pre, n + 1u)][bucket(n)], 1u);
+      pre += n + 1u;
+    }
+  }
+  __syncthreads();
+  // 3. per band, the exclusive scan of its 1024 bucket counts (the existing k_tile_order scan, once per band)
+  for (int g = 0; g < XG; ++g) {
+    const uint32_t v = s_cnt[g][tid];
+    uint32_t inc32 = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc32, o, 64);
+      if (lane >= o) inc32 += y;
+    }
+    if (lane == 63) s_w32[w] = inc32;
+    __syncthreads();
+    uint32_t wbase = 0u, tot = 0u;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) wbase += s_w32[k];
+      tot += s_w32[k];
+    }
+    s_cnt[g][tid] = wbase + inc32 - v;
+    if (tid == 0) s_n[g] = tot;
+    __syncthreads();
+  }
+  // 4. each tile's rank in its band -> its block
+  uint32_t m = s_n[0];
+#pragma unroll
+  for (int g = 1; g < XG; ++g) m = min(m, s_n[g]);
+  unsigned long long pre = before;
+  for (int t = t0; t < t1; ++t) {
+    const uint32_t n = len(t);
+    const int g = band(pre, n + 1u);
+    pre += n + 1u;
+    const uint32_t r = atomicAdd(&s_cnt[g][bucket(n)], 1u);
+    uint32_t b;
+    if (r < m) {
+      b = r * XG + (uint32_t)g;
+    } else {
+      b = m * XG + (r - m);
+      for (int h = 0; h < g; ++h) b += s_n[h] - m;
+    }
+    order[b] = (uint32_t)t;
+  }
+}
+
+// the launch order of a tile pass: by the LM product's modelled cost (cost != NULL) k_tile_order_xcd, unless
+// GSLM_TILE_ORDER=flat (A/B); by list length (the forward, the loss blends) the frame-wide k_tile_order -- banded by
+// length the blends ran 11-15% slower (profiles/r05/ab/tile_order_xcd_lm_kept/): a list's length does not price a
+// blend that stops at T < 1e-4, so equal-length bands are unequal work for their XCDs, while the modelled cost does
+static bool tile_order_xcd() {
+  static const bool on = [] {
+    const char* e = getenv("GSLM_TILE_ORDER");
+    return !(e && std::string(e) == "flat");
+  }();
+  return on;
+}
+int launch_tile_order(int ntiles, const uint2* ranges, uint32_t* order, const uint32_t* cost, hipStream_t s) {
+  if (cost && tile_order_xcd())
+    hipLaunchKernelGGL(k_tile_order_xcd, dim3(1), dim3(1024), 0, s, ntiles, ranges, order, cost);
+  else
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, ranges, order, cost);
+  GSLM_LAUNCH_CHECK();
+  return GSLM_OK;
+}
+
 // Gaussian ids of the sorted list (mask bits stripped), for gslm_inspect.
 __global__ __launch_bounds__(256) void k_point_ids(int64_t N, const uint32_t* __restrict__ pl, uint32_t* __restrict__ out) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -514,7 +626,7 @@ int launch_lm_rowmap(const ViewK& v, const GeomBufs& gb, const BinBufs& bb, cons
     // the LM tile passes' launch order by their modelled cost (hscan holds the costs until k_row_flags rewrites it;
     // only the schedule changes, every tile's results are independent of when it runs)
     hipLaunchKernelGGL(k_tile_cost, dim3(ntiles), dim3(256), 0, s, bb.ranges, bb.point_list, bb.tile_neff, sb.hscan);
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, sb.hscan);
+    if (int st = launch_tile_order(ntiles, bb.ranges, bb.tile_order, sb.hscan, s)) return st;
   }
   hipLaunchKernelGGL(k_row_flags, dim3(nb), dim3(256), 0, s, N, v.gx, bb.keys_sorted, bb.point_list, bb.ranges,
                      bb.tile_neff, gb.goff, gb.rect, bb.slots, sb.hscan);
@@ -720,7 +832,7 @@ int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const Bi
                        (uint32_t*)nullptr);
     GSLM_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
+  if (int st = launch_tile_order(ntiles, bb.ranges, bb.tile_order, nullptr, s)) return st;
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -781,7 +893,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
       if (P > 0) GSLM_HIP_CHECK(hipMemcpyAsync(n_out, gb.counters, 4, hipMemcpyDeviceToDevice, s));
       else GSLM_HIP_CHECK(hipMemsetAsync(n_out, 0, 4, s));
     }
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
+    if (int st = launch_tile_order(ntiles, bb.ranges, bb.tile_order, nullptr, s)) return st;
     GSLM_LAUNCH_CHECK();
     return GSLM_OK;
   }
@@ -796,7 +908,7 @@ int launch_binning(const ViewK& v, int64_t P, const GeomBufs& gb, const BinBufs&
   const unsigned nbN = (unsigned)((N + 256 * RANGES_KEYS - 1) / (256 * RANGES_KEYS));
   hipLaunchKernelGGL(k_ranges, dim3(nbN), dim3(256), 0, s, N, bb.keys_sorted, bb.ranges, n_dev, n_out);
   GSLM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ntiles, bb.ranges, bb.tile_order, nullptr);
+  if (int st = launch_tile_order(ntiles, bb.ranges, bb.tile_order, nullptr, s)) return st;
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
