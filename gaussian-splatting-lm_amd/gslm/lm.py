@@ -1086,12 +1086,15 @@ class LossEvaluator:
                     check(lib.gslm_depth_positions(self._orders[i].data_ptr(), P, self._pos[i].data_ptr(), main_h),
                           "gslm_depth_positions")
             # 2. the sets' render records in depth space: one pass over the Gaussians per set for the batch's views
-            vws = (_lib.GslmView * len(idx))(*[self.views[i] for i in idx])
-            pos = (ctypes.c_void_p * len(idx))(*[self._pos[i].data_ptr() for i in idx])
-            for a in range(n):
-                ge = (ctypes.c_void_p * len(idx))(*[sl["geoms"][a].data_ptr() for sl in slots])
-                check(lib.gslm_preprocess_views(vws, len(idx), ctypes.byref(gs[a]), ge, slots[0]["geoms"][a].numel(),
-                                                pos, main_h), "gslm_preprocess_views")
+            # (gslm_preprocess_views takes at most 8 views per call: a batch above 8 goes in chunks)
+            for c0 in range(0, len(idx), 8):
+                cidx = idx[c0:c0 + 8]
+                vws = (_lib.GslmView * len(cidx))(*[self.views[i] for i in cidx])
+                pos = (ctypes.c_void_p * len(cidx))(*[self._pos[i].data_ptr() for i in cidx])
+                for a in range(n):
+                    ge = (ctypes.c_void_p * len(cidx))(*[sl["geoms"][a].data_ptr() for sl in slots[c0:c0 + 8]])
+                    check(lib.gslm_preprocess_views(vws, len(cidx), ctypes.byref(gs[a]), ge,
+                                                    slots[0]["geoms"][a].numel(), pos, main_h), "gslm_preprocess_views")
             # 3. union geometries and their pair counts (main stream; the read-back waits for main only)
             for k, i in enumerate(idx):
                 ge = (ctypes.c_void_p * n)(*[slots[k]["geoms"][a].data_ptr() for a in range(n)])

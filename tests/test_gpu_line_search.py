@@ -88,6 +88,18 @@ def test_evaluate_points_equal_exact_renders(batch, streams):
     assert [float(x) for x in ev_u.evaluate_points(sets2)] == exact2
 
 
+def test_evaluate_points_batch_above_eight_views():
+    """A batch of more views than one gslm_preprocess_views call takes (8): the batch's depth-space preprocesses go in
+    chunks of 8 (lm_step(val_batch=12) raised before round 5's fix)."""
+    from gslm.lm import LossEvaluator
+    m, cams = _scene(P=5000, nviews=11)
+    lay, s = _step(m)
+    ev_x = LossEvaluator(m, cams, torch.zeros(3), batch=11, streams=3)
+    ev_u = LossEvaluator(m, cams, torch.zeros(3), batch=11, streams=3)
+    sets, exact, _, _ = _points(m, lay, s, ev_x)
+    assert [float(x) for x in ev_u.evaluate_points(sets)] == exact
+
+
 @pytest.mark.parametrize("D", [0, 1])
 def test_evaluate_points_equal_exact_renders_low_sh_degree(D):
     """SH degree 0 (no SH-rest leaf: the preprocess cannot stage SH rows and runs its unstaged form, which must still
