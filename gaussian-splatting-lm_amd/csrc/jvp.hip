@@ -164,6 +164,9 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
       }
     }
     uint64_t hb = __ballot(hit);
+    // pos = base + j < my_last as j < my_last - base: the lane's bound once per round, the hit's index compared as
+    // the SGPR it is (no scalar add per visit)
+    const int rel = (int)my_last - base;
     wave_lds_sync();
     while (hb) {
       const int j = (int)__builtin_ctzll(hb);
@@ -171,12 +174,11 @@ __device__ __forceinline__ void jvp_wave_packed(JvpPix& o, float pxf, float pyf,
       const float4 a = s[j], b = s[64 + j], C = s[128 + j], D = s[192 + j];
       asm volatile("" : : "v"(b.z), "v"(b.w), "v"(C.x), "v"(C.y), "v"(C.z), "v"(C.w), "v"(D.x), "v"(D.y), "v"(D.z),
                    "v"(D.w));
-      const uint32_t pos = (uint32_t)(base + j);
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = gpower(a.z, a.w, b.x, dx, dy);
       const float G = gexp(power);
       const float alpha = fminf(0.99f, b.y * G);
-      if (pos < my_last && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
+      if (j < rel && !(power > 0.0f) && alpha >= 1.0f / 255.0f) {
 #pragma clang fp contract(fast)
         const float dpower = fmaf(dx, fmaf(C.y, dx, C.z * dy), C.w * dy * dy);  // 5 VALU, not 6
         const float dalpha = G * (D.x + b.y * dpower);
