@@ -67,8 +67,7 @@ __global__ __launch_bounds__(DOT_THREADS) void k_dot_partial(const float* __rest
 __global__ __launch_bounds__(DOT_THREADS) void k_dot_final(const double* __restrict__ part, int np,
                                                            double* __restrict__ out) {
   __shared__ double s[DOT_THREADS / 64];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += DOT_THREADS) acc += part[i];
+  const double acc = strided_sum_in_order(part, np);
   const double t = block_sum_d(acc, s);
   if (threadIdx.x == 0) *out = t;
 }

@@ -54,6 +54,25 @@ struct ViewK {
 // torch.clamp(x, 0, 1) (the reference's rendered_image.clamp(0, 1), batch_render.py:118): a NaN stays a NaN, as in
 // torch -- fminf / fmaxf would turn it into 0 or 1 and hide it from the reference's NaN asserts (solver_functions.py:
 // 125-130).  Identical to fminf(fmaxf(x, 0), 1) for every other input.
+// Thread-strided in-order sum ((x[t] + x[t + T]) + x[t + 2T]) + ... (T = blockDim.x) with the loads issued 8 at a
+// time: one memory latency per 8 partials, where the one-at-a-time loop waited on every load.  The additions keep
+// that loop's order (a skipped slot adds nothing), so the sum is bitwise the same -- the deterministic reductions'
+// contract.
+template <typename F>
+__device__ __forceinline__ F strided_sum_in_order(const F* __restrict__ x, int64_t n) {
+  F acc = F(0);
+  const int64_t T = blockDim.x;
+  for (int64_t i = threadIdx.x; i < n; i += 8 * T) {
+    F v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = i + k * T < n ? x[i + k * T] : F(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i + k * T < n) acc += v[k];
+  }
+  return acc;
+}
+
 __device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
 
 // block-uniform early exit of a product kernel once the device-side CG stopping tests fired

@@ -265,8 +265,7 @@ __global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __re
                                                                LossPtrsK lp) {
   __shared__ double s[4];
   const int a = blockIdx.x;
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) acc += part[(int64_t)a * np + i];
+  double acc = strided_sum_in_order(part + (int64_t)a * np, np);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
@@ -312,8 +311,7 @@ __global__ __launch_bounds__(256) void k_tile_loss_final(const double* __restric
                                                           double* __restrict__ loss, const uint32_t* __restrict__ nsets,
                                                           int slot) {
   __shared__ double s[4];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  double acc = strided_sum_in_order(part, np);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;

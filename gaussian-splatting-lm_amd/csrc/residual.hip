@@ -55,8 +55,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_lm_residual(int64_t HW, const f
 __global__ __launch_bounds__(RES_THREADS) void k_lm_loss_final(const double* __restrict__ part, int np, int accumulate,
                                                                double* __restrict__ loss) {
   __shared__ double s[RES_THREADS / 64];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += RES_THREADS) acc += part[i];
+  double acc = strided_sum_in_order(part, np);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);

@@ -163,8 +163,7 @@ __global__ __launch_bounds__(256) void k_ssim_eval(SsimWin w, int H, int W, floa
 __global__ __launch_bounds__(256) void k_ssim_loss_final(const double* __restrict__ part, int np, int accumulate,
                                                          double* __restrict__ loss) {
   __shared__ double s[4];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  double acc = strided_sum_in_order(part, np);
   const double t = block_sum_256(acc, s);
   if (threadIdx.x == 0) *loss = accumulate ? *loss + t : t;
 }
@@ -254,8 +253,7 @@ __global__ __launch_bounds__(256) void k_ssim_mean(SsimWin w, int H, int W, int 
 __global__ __launch_bounds__(256) void k_ssim_mean_final(const double* __restrict__ part, int np, double inv_n,
                                                          float* __restrict__ out) {
   __shared__ double s[4];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  double acc = strided_sum_in_order(part, np);
   const double t = block_sum_256(acc, s);
   if (threadIdx.x == 0) *out = (float)(t * inv_n);
 }
