@@ -53,8 +53,7 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
 // block's threads (b <= a few thousand: L2-resident loads).  In the apply pass this replaces the scan-of-block-sums
 // launch between the two passes (a single-block kernel at its ~5 us floor, twice per forward).
 __device__ __forceinline__ uint32_t block_sums_before(const uint32_t* __restrict__ bs, int b, uint32_t* s_w) {
-  uint32_t acc = 0;
-  for (int i = threadIdx.x; i < b; i += blockDim.x) acc += bs[i];
+  const uint32_t acc = strided_sum_in_order(bs, b);  // loads 8 deep
   uint32_t tot;
   block_incl_scan256(acc, s_w, &tot);
   return tot;
