@@ -87,13 +87,25 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
   const int d = blockIdx.x, tid = threadIdx.x;
   uint32_t* h = hist + (int64_t)d * nblocks;
   uint32_t carry = 0;
-  for (int base = 0; base < nblocks; base += 256) {
-    const int i = base + tid;
-    const uint32_t x = i < nblocks ? h[i] : 0u;
-    uint32_t tot;
-    const uint32_t inc = block_incl_scan256(x, s_w, &tot);
-    if (i < nblocks) h[i] = carry + inc - x;
-    carry += tot;
+  // up to 8 chunks of 256 counts loaded together (the tile sort's ~1200 blocks: 5 chunks, one load latency instead of
+  // five), then scanned chunk by chunk; each count is read before its own slot is rewritten
+  for (int base0 = 0; base0 < nblocks; base0 += 8 * 256) {
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = base0 + k * 256 + tid;
+      x[k] = i < nblocks ? h[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int base = base0 + k * 256;
+      if (base >= nblocks) break;  // block-uniform
+      const int i = base + tid;
+      uint32_t tot;
+      const uint32_t inc = block_incl_scan256(x[k], s_w, &tot);
+      if (i < nblocks) h[i] = carry + inc - x[k];
+      carry += tot;
+    }
   }
   if (tid == 0) totals[d] = carry;
 }
