@@ -72,6 +72,18 @@ __global__ __launch_bounds__(DOT_THREADS) void k_dot_final(const double* __restr
   if (threadIdx.x == 0) *out = t;
 }
 
+// The monitor's three finalisations (γ', <x, g>, <x, s>) in one launch: block b sums part + b np into its output,
+// bitwise as three k_dot_final launches.
+__global__ __launch_bounds__(DOT_THREADS) void k_dot_final3(const double* __restrict__ part, int np,
+                                                            double* __restrict__ o0, double* __restrict__ o1,
+                                                            double* __restrict__ o2) {
+  __shared__ double s[DOT_THREADS / 64];
+  const int b = blockIdx.x;
+  const double acc = strided_sum_in_order(part + (int64_t)b * np, np);
+  const double t = block_sum_d(acc, s);
+  if (threadIdx.x == 0) *(b == 0 ? o0 : (b == 1 ? o1 : o2)) = t;
+}
+
 __global__ __launch_bounds__(256) void k_axpy_dev(int64_t n, const double* __restrict__ num,
                                                   const double* __restrict__ den, float sign,
                                                   const float* __restrict__ x, float* __restrict__ y) {
@@ -266,9 +278,7 @@ int gslm_cg_update_monitor(int64_t n, const double* gam_dev, const double* del_d
   const double* part = (const double*)scratch;
   hipLaunchKernelGGL(k_cg_update<true>, dim3(DOT_BLOCKS), dim3(DOT_THREADS), 0, st, n, gam_dev, del_dev, p, q, x, s, g,
                      (double*)scratch, cg_ctl);
-  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part, DOT_BLOCKS, gam_new_dev);
-  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + DOT_BLOCKS, DOT_BLOCKS, xg_dev);
-  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(DOT_THREADS), 0, st, part + 2 * DOT_BLOCKS, DOT_BLOCKS, xs_dev);
+  hipLaunchKernelGGL(k_dot_final3, dim3(3), dim3(DOT_THREADS), 0, st, part, DOT_BLOCKS, gam_new_dev, xg_dev, xs_dev);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
