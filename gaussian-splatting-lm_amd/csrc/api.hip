@@ -534,8 +534,9 @@ int gslm_rasterize_loss_sets(const gslm_view* view, int64_t P, const void* const
   UnionMasks um;
   bin_layout(N, v.gx * v.gy, const_cast<void*>(binning), &bb);
   union_masks_layout(N, v.gx * v.gy, const_cast<void*>(binning), &um);
+  // um.nsets: slots at or past the set count gslm_union_binning recorded render a NaN loss (as the slot form)
   return launch_render_loss_sets(v, sr, n, bb, um.sorted, gt, alpha_mask, (double*)scratch, lp, accumulate ? 1 : 0,
-                                 (hipStream_t)stream, first_set);
+                                 (hipStream_t)stream, first_set, um.nsets);
 }
 
 int gslm_num_rendered_copy(const void* geom, int64_t P, uint32_t* dst, void* stream) {

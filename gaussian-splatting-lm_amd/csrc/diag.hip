@@ -27,3 +27,17 @@ extern "C" int gslm_selftest(int32_t which, const float* in, float* out, void* s
   }
   return GSLM_OK;
 }
+
+extern "C" int gslm_selftest_scan(const uint32_t* in, uint32_t* out, int64_t n, int32_t force_top, void* tmp,
+                                  size_t tmp_bytes, uint32_t* total, void* stream) {
+  if (n < 0 || (n > 0 && (!in || !out || !tmp || !total))) {
+    gslm::set_error("selftest_scan: n < 0 or NULL buffer");
+    return GSLM_ERR_INVALID;
+  }
+  if (tmp_bytes < gslm::scan_tmp_bytes(n)) {
+    gslm::set_error("selftest_scan: tmp below 8 ceil(n / 2048) + 64 bytes");
+    return GSLM_ERR_CAPACITY;
+  }
+  return gslm::exclusive_scan_u32(in, nullptr, out, n, static_cast<uint32_t*>(tmp), total, (hipStream_t)stream,
+                                  force_top ? 0 : gslm::SCAN_INLINE_MAX_BLOCKS);
+}

@@ -93,10 +93,18 @@ constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = GSLM_SCAN_ITEMS;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 inline int64_t scan_blocks(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+// Above this many blocks a scan's apply pass no longer sums its prefix of block sums itself (O(nb^2) loads over the
+// grid) but reads it from a scanned copy (k_scan_top, one more launch).  The bench's forward scans (1M Gaussians,
+// nb = 489) and its LM row map (4.87M pairs, nb = 2377) keep the two-launch form.
+#ifndef GSLM_SCAN_INLINE_MAX_BLOCKS
+#define GSLM_SCAN_INLINE_MAX_BLOCKS 4096
+#endif
+constexpr int64_t SCAN_INLINE_MAX_BLOCKS = GSLM_SCAN_INLINE_MAX_BLOCKS;
 inline size_t scan_tmp_bytes(int64_t n) { return align_up((size_t)scan_blocks(n) * 8 + 64); }  // dual scans: 2 nb
 // out[i] = sum_{j<i} in[idx ? idx[j] : j];  *total (device) = full sum.
+// inline_max_blocks: the largest block count whose apply pass sums its own prefix of block sums (above it, k_scan_top)
 int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
-                       uint32_t* total, hipStream_t s);
+                       uint32_t* total, hipStream_t s, int64_t inline_max_blocks = SCAN_INLINE_MAX_BLOCKS);
 // out_a[i] = sum_{j<i} in[j], out_b[i] = sum_{j<i} b[j] in one pass (tmp: scan_tmp_bytes(n)), b = in_b, or in
 // gathered through idx when in_b is NULL.
 int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* out_a, uint32_t* out_b, int64_t n,

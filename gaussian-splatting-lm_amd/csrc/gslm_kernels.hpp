@@ -532,7 +532,7 @@ struct LossPtrsK {
 };
 int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const BinBufs& bb, const uint32_t* amask,
                             const float* gt, const float* mask, double* part, const LossPtrsK& lp, int accumulate,
-                            hipStream_t s, int first_set = 0);
+                            hipStream_t s, int first_set = 0, const uint32_t* nsets_dev = nullptr);
 int launch_union_rect(int64_t P, const UnionSets& u, const GeomBufs& ug, hipStream_t s);
 int launch_depth_positions(int64_t P, const uint32_t* order, uint32_t* pos, hipStream_t s);
 int launch_union_binning(const ViewK& v, int64_t P, const GeomBufs& ug, const BinBufs& bb, const UnionMasks& um,

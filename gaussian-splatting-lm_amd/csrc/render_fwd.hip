@@ -260,9 +260,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NS <= 6 ? 8
   if (tid < NS) part[(int64_t)tid * (v.gx * v.gy) + tile] = ((s_sum[tid][0] + s_sum[tid][1]) + s_sum[tid][2]) + s_sum[tid][3];
 }
 
-// per set a (block a): the sum of its per-tile partials in tile order, times 2, into *loss[a] (k_tile_loss_final)
+// per set a (block a): the sum of its per-tile partials in tile order, times 2, into *loss[a] (k_tile_loss_final);
+// nsets (or NULL): the union binning's recorded set count -- slot first_set + a at or past it (masks that were never
+// built) gets a NaN loss, as gslm_rasterize_loss_slot gives it
 __global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __restrict__ part, int np, int accumulate,
-                                                               LossPtrsK lp) {
+                                                               LossPtrsK lp, const uint32_t* __restrict__ nsets,
+                                                               int first_set) {
   __shared__ double s[4];
   const int a = blockIdx.x;
   double acc = strided_sum_in_order(part + (int64_t)a * np, np);
@@ -271,7 +274,8 @@ __global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __re
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    double l = 2.0 * (((s[0] + s[1]) + s[2]) + s[3]);
+    if (nsets && (uint32_t)(first_set + a) >= *nsets) l = __longlong_as_double(0x7ff8000000000000ll);  // quiet NaN
     double* out = lp.loss[a];
     *out = accumulate ? *out + l : l;
   }
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(256) void k_tile_loss_final_sets(const double* __re
 
 int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const BinBufs& bb, const uint32_t* amask,
                             const float* gt, const float* mask, double* part, const LossPtrsK& lp, int accumulate,
-                            hipStream_t s, int first_set) {
+                            hipStream_t s, int first_set, const uint32_t* nsets_dev) {
   const int ntiles = v.gx * v.gy;
   if (ntiles == 0) {
     if (!accumulate)
@@ -300,7 +304,8 @@ int launch_render_loss_sets(const ViewK& v, const SetRecsK& sr, int nsets, const
       set_error("rasterize_loss_sets: 1..8 parameter sets");
       return GSLM_ERR_INVALID;
   }
-  hipLaunchKernelGGL(k_tile_loss_final_sets, dim3(nsets), dim3(256), 0, s, (const double*)part, ntiles, accumulate, lp);
+  hipLaunchKernelGGL(k_tile_loss_final_sets, dim3(nsets), dim3(256), 0, s, (const double*)part, ntiles, accumulate, lp,
+                     amask ? nsets_dev : nullptr, first_set);
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -50,13 +50,44 @@ __device__ __forceinline__ uint32_t block_incl_scan256(uint32_t x, uint32_t* s_w
 }
 
 // The exclusive prefix of the first b of a scan's per-block sums (written raw by the reduce pass), summed by the
-// block's threads (b <= a few thousand: L2-resident loads).  In the apply pass this replaces the scan-of-block-sums
-// launch between the two passes (a single-block kernel at its ~5 us floor, twice per forward).
+// block's threads (b <= SCAN_INLINE_MAX_BLOCKS: L2-resident loads).  In the apply pass this replaces the
+// scan-of-block-sums launch between the two passes (a single-block kernel at its ~5 us floor, twice per forward).
+// The loads grow as nb^2 / 2 over the grid, so longer scans (the LM row map over N pairs at 5M Gaussians or 4K frames:
+// nb ~ 12k-49k) scan the block sums in a launch of their own (k_scan_top, SCANNED = true) and read their prefix.
+template <bool SCANNED>
 __device__ __forceinline__ uint32_t block_sums_before(const uint32_t* __restrict__ bs, int b, uint32_t* s_w) {
+  if (SCANNED) return bs[b];
   const uint32_t acc = strided_sum_in_order(bs, b);  // loads 8 deep
   uint32_t tot;
   block_incl_scan256(acc, s_w, &tot);
   return tot;
+}
+
+// One block per sequence of nb block sums (bs + blockIdx.x * nb): in-place exclusive scan, chunks of 8 x 256 loaded
+// together (as k_radix_scan).
+__global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ bs, int nb) {
+  __shared__ uint32_t s_w[4];
+  uint32_t* h = bs + (int64_t)blockIdx.x * nb;
+  const int tid = threadIdx.x;
+  uint32_t carry = 0;
+  for (int base0 = 0; base0 < nb; base0 += 8 * 256) {
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = base0 + k * 256 + tid;
+      x[k] = i < nb ? h[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int base = base0 + k * 256;
+      if (base >= nb) break;  // block-uniform
+      const int i = base + tid;
+      uint32_t tot;
+      const uint32_t inc = block_incl_scan256(x[k], s_w, &tot);
+      if (i < nb) h[i] = carry + inc - x[k];
+      carry += tot;
+    }
+  }
 }
 
 // n_dev (or NULL): the key count is min(n, *n_dev), read on the device (a capacity-sized launch whose count the host
@@ -240,13 +271,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* __
 
 // In-place form of k_scan_apply (data = in = out, no index gather): one pointer without __restrict__, so the
 // compiler keeps every thread's loads of its elements ahead of its stores to them.
+template <bool SCANNED>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* data, int64_t n,
                                                                      const uint32_t* __restrict__ block_sums,
                                                                      uint32_t* __restrict__ total) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
-  const uint32_t before = block_sums_before(block_sums, blockIdx.x, s_w);
+  const uint32_t before = block_sums_before<SCANNED>(block_sums, blockIdx.x, s_w);
   uint32_t v[SCAN_ITEMS];
   uint32_t acc = 0;
 #pragma unroll
@@ -267,6 +299,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply_inplace(uint32_t* d
   }
 }
 
+template <bool SCANNED>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __restrict__ in,
                                                              const uint32_t* __restrict__ idx, int64_t n,
                                                              const uint32_t* __restrict__ block_sums,
@@ -274,7 +307,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint32_t* __r
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
-  const uint32_t before = block_sums_before(block_sums, blockIdx.x, s_w);
+  const uint32_t before = block_sums_before<SCANNED>(block_sums, blockIdx.x, s_w);
   uint32_t v[SCAN_ITEMS];
   uint32_t acc = 0;
 #pragma unroll
@@ -323,6 +356,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_reduce(const uint32_t* _
   }
 }
 
+template <bool SCANNED>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __restrict__ in,
                                                               const uint32_t* __restrict__ idx,
                                                               const uint32_t* __restrict__ in_b, int64_t n,
@@ -333,8 +367,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan2_apply(const uint32_t* __
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
-  const uint32_t before_a = block_sums_before(block_sums, blockIdx.x, s_w);
-  const uint32_t before_b = block_sums_before(block_sums + gridDim.x, blockIdx.x, s_w);
+  const uint32_t before_a = block_sums_before<SCANNED>(block_sums, blockIdx.x, s_w);
+  const uint32_t before_b = block_sums_before<SCANNED>(block_sums + gridDim.x, blockIdx.x, s_w);
   uint32_t va[SCAN_ITEMS], vb[SCAN_ITEMS];
   uint32_t acc_a = 0, acc_b = 0;
 #pragma unroll
@@ -377,8 +411,14 @@ int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* o
   }
   const int nb = (int)scan_blocks(n);
   hipLaunchKernelGGL(k_scan2_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp);
-  hipLaunchKernelGGL(k_scan2_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b, total_a,
-                     total_b);
+  if (nb > SCAN_INLINE_MAX_BLOCKS) {
+    hipLaunchKernelGGL(k_scan_top, dim3(2), dim3(256), 0, s, tmp, nb);
+    hipLaunchKernelGGL(k_scan2_apply<true>, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b,
+                       total_a, total_b);
+  } else {
+    hipLaunchKernelGGL(k_scan2_apply<false>, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, in_b, n, tmp, out_a, out_b,
+                       total_a, total_b);
+  }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }
@@ -432,17 +472,22 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
 }
 
 int exclusive_scan_u32(const uint32_t* in, const uint32_t* idx, uint32_t* out, int64_t n, uint32_t* tmp,
-                       uint32_t* total, hipStream_t s) {
+                       uint32_t* total, hipStream_t s, int64_t inline_max_blocks) {
   if (n <= 0) {
     GSLM_HIP_CHECK(hipMemsetAsync(total, 0, 4, s));
     return GSLM_OK;
   }
   const int nb = (int)scan_blocks(n);
   hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp);
-  if (out == in && !idx)  // in place (the LM row map's head-flag scan)
-    hipLaunchKernelGGL(k_scan_apply_inplace, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp, total);
-  else
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out, total);
+  const bool top = nb > inline_max_blocks;
+  if (top) hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, tmp, nb);
+  if (out == in && !idx) {  // in place (the LM row map's head-flag scan)
+    if (top) hipLaunchKernelGGL(k_scan_apply_inplace<true>, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp, total);
+    else hipLaunchKernelGGL(k_scan_apply_inplace<false>, dim3(nb), dim3(SCAN_THREADS), 0, s, out, n, tmp, total);
+  } else {
+    if (top) hipLaunchKernelGGL(k_scan_apply<true>, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out, total);
+    else hipLaunchKernelGGL(k_scan_apply<false>, dim3(nb), dim3(SCAN_THREADS), 0, s, in, idx, n, tmp, out, total);
+  }
   GSLM_LAUNCH_CHECK();
   return GSLM_OK;
 }

@@ -799,6 +799,25 @@ def cgls_residual(prob, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, verbo
     return x, {"iters": iter_total, "residuals": history}
 
 
+def loss_set_group():
+    """Sets per blend pass of the line search (GSLM_LOSS_SET_GROUP, 1..8; default 1 = one pass per set).
+
+    The variable was GSLM_LOSS_SETS until round 5, whose meaning changed between rounds (round 4: 1 = all sets; round
+    5: 1 = per set): the old spelling is refused rather than silently read with either meaning, and so is a value
+    outside 1..8."""
+    if "GSLM_LOSS_SETS" in os.environ:
+        raise ValueError("GSLM_LOSS_SETS is no longer read: set GSLM_LOSS_SET_GROUP=k (k sets per blend pass, 1..8; "
+                         "1 = per set, the default; 8 = all sets in one pass)")
+    raw = os.environ.get("GSLM_LOSS_SET_GROUP", "1")
+    try:
+        k = int(raw)
+    except ValueError:
+        k = 0
+    if not 1 <= k <= 8:
+        raise ValueError(f"GSLM_LOSS_SET_GROUP={raw!r}: sets per blend pass must be an integer in 1..8")
+    return k
+
+
 class LossEvaluator:
     """The line search's validation loss: `val_loss_func().loss_scalar` of train_jvp.py:258,268,279 (batch_training_loss
     with disable_ssim=True over the validation views: 2 sum_b ||m_b clamp01(R_b) - gt_b||^2) on the HIP forward.
@@ -859,9 +878,9 @@ class LossEvaluator:
         # passes over groups of loss_sets sets each (gslm_rasterize_loss_sets) -- the same losses bitwise.  Per set is
         # the default: the all-sets pass wins when evaluate_points runs back to back (69.8 against 74.8 ms for the six
         # points over 50 views) but not inside lm_step, where it holds the CUs longer against the next batch's sorts
-        # on the other streams (profiles/r04/ab/all_sets_default/, profiles/r05/ab/loss_set_groups/).  GSLM_LOSS_SETS=k
-        # selects groups of k (1 = per set; the round-4 GSLM_LOSS_SETS=1 meaning "all sets" is k = 8).
-        self.loss_sets = max(1, min(8, int(os.environ.get("GSLM_LOSS_SETS", "1"))))
+        # on the other streams (profiles/r04/ab/all_sets_default/, profiles/r05/ab/loss_set_groups/).
+        # GSLM_LOSS_SET_GROUP=k (1..8) selects groups of k (1 = per set, 8 = all sets in one pass).
+        self.loss_sets = loss_set_group()
         self.union_counts = []
 
     def _slot(self, k, P):

@@ -557,6 +557,11 @@ int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t num_r
  * which = 0: transposed 8-value reduction (lane l returns the sum of value (l >> 3) & 7);
  * which = 1: DPP sum of in[l*8] (lane 63 returns the total). */
 int gslm_selftest(int32_t which, const float* in, float* out, void* stream);
+/* Device self-test of the library's exclusive u32 scan (the tile-count and LM row-map scans): out[i] = sum_{j<i} in[j],
+ * *total = the sum (both device).  force_top != 0 takes the long-scan form (a scan of the block sums in a launch of
+ * its own, used above 4096 blocks of 2048) at any n.  tmp: >= 8 ceil(n / 2048) + 64 bytes of device scratch. */
+int gslm_selftest_scan(const uint32_t* in, uint32_t* out, int64_t n, int32_t force_top, void* tmp, size_t tmp_bytes,
+                       uint32_t* total, void* stream);
 
 const char* gslm_last_error(void);
 int gslm_abi_version(void);

@@ -250,3 +250,23 @@ def test_comm_entry_points_check_arguments():
     assert lib.gslm_allgather(None, None, None, 16, None) == -1
     assert b"NULL" in lib.gslm_last_error()
     assert lib.gslm_comm_destroy(None) == 0
+
+
+def test_loss_set_group_env_is_validated(monkeypatch):
+    """the line search's sets-per-blend-pass knob is GSLM_LOSS_SET_GROUP (1..8); the round-4/5 spelling
+    GSLM_LOSS_SETS, whose meaning changed between those rounds, is refused, and so are out-of-range values."""
+    from gslm.lm import loss_set_group
+    monkeypatch.delenv("GSLM_LOSS_SETS", raising=False)
+    monkeypatch.delenv("GSLM_LOSS_SET_GROUP", raising=False)
+    assert loss_set_group() == 1
+    for k in (1, 3, 8):
+        monkeypatch.setenv("GSLM_LOSS_SET_GROUP", str(k))
+        assert loss_set_group() == k
+    for bad in ("0", "9", "-1", "all", ""):
+        monkeypatch.setenv("GSLM_LOSS_SET_GROUP", bad)
+        with pytest.raises(ValueError):
+            loss_set_group()
+    monkeypatch.setenv("GSLM_LOSS_SET_GROUP", "2")
+    monkeypatch.setenv("GSLM_LOSS_SETS", "1")
+    with pytest.raises(ValueError, match="GSLM_LOSS_SET_GROUP"):
+        loss_set_group()

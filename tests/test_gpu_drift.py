@@ -11,24 +11,28 @@ rounding.
 What is asserted (round 5, VERDICT r04 "make the parity bounds measure correctness, not rounding luck"): the quantities
 the solve is FOR, scale-free, over three ground truths (perturbation seeds), both layouts --
   * the LM model decrease m(x) = 1/2 x^T A x - g^T x, which CG lowers monotonically: the float32 solve's m after 10
-    iterations must lie within ONE iteration's progress of the float64 recursion's (|m32 - m64[10]| <= m64[9] -
-    m64[10]).  Neither recursion is exact -- the operator is applied in float32 -- and at this conditioning either may
+    iterations, lag = (m32 - m64[10]) / (m64[9] - m64[10]) in units of the float64 recursion's tenth-iteration
+    decrease.  Neither recursion is exact -- the operator is applied in float32 -- and at this conditioning either may
     end up ahead (round 5, seed 9: the float32 solve's m is 7.6% of an iteration BELOW the float64 one's, and its
-    residual 25% lower); lag = (m32 - m64[10]) / (m64[9] - m64[10]) is logged, |lag| <= 1 asserted;
-  * the normal-equation residual rho(x) = |g - A x| / |g|: logged, held to a gross-error guard (rho32 < 1, within 2x
-    of rho64) -- measured as unstable as the iterate itself (the 25% above), so it cannot carry a tight bound.
-The iterate drift |x32 - x64| / |x64| is REPORTED (and held to a gross-error guard only): after 10 iterations at 1M it
-reflects the conditioning of the iterates -- round 4 saw it move 12x (2.6e-4 -> 3.2e-3) under one extra rounding in
-the exponent while rho and m did not move (profiles/r04/ab/rec_conic_log2e_rejected/).  Every value goes to the parity
-margin log (tests/margins.py).
+    residual 25% lower).  The bound is ONE-SIDED (round 6): the float32 solve may be ahead (lag < 0)
+    by up to a whole iteration (a gross-error guard: being further ahead than the float64 recursion's last step would
+    mean the two recursions do not solve the same system), and BEHIND (lag > 0) by at most LAG_BEHIND = 0.25 of an
+    iteration (worst measured behind: +0.015; the log2e-perturbed build: +0.022);
+  * the normal-equation residual rho(x) = |g - A x| / |g|: logged, held to a guard (rho32 < 1, within RHO_GUARD of
+    rho64; worst measured 0.246) -- measured as unstable as the iterate itself (the 25% above).
+The iterate drift |x32 - x64| / |x64| is REPORTED and held to DRIFT_GUARD (worst measured 8.2e-3, full layout): after 10
+iterations at 1M it reflects the conditioning of the iterates -- round 4 saw it move 12x (2.6e-4 -> 3.2e-3) under one
+extra rounding in the exponent while rho and m did not move (profiles/r04/ab/rec_conic_log2e_rejected/).  Every value
+goes to the parity margin log (tests/margins.py).
 """
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
-LAG_TOL = 1.0       # |m32 - m64[10]| / (m64[9] - m64[10]): within one iteration's progress
-RHO_GUARD = 1.0     # |rho32 - rho64| / rho64, a gross-error guard (reported)
-DRIFT_GUARD = 5e-2  # the iterate drift, reported; this bound only catches gross errors
+LAG_BEHIND = 0.25   # (m32 - m64[10]) / (m64[9] - m64[10]) <= this: behind by at most a quarter iteration
+LAG_AHEAD = 1.0     # ... >= -this: ahead by at most one iteration (gross-error guard)
+RHO_GUARD = 0.5     # |rho32 - rho64| / rho64 (worst measured 0.246)
+DRIFT_GUARD = 2e-2  # the iterate drift (worst measured 8.2e-3)
 SEEDS = (2, 5, 9)
 
 
@@ -108,10 +112,12 @@ def test_cg_against_float64_recursion_at_bench_size(seed):
         lag = (m32 - mh[10]) / (mh[9] - mh[10])
         print(f"seed {seed} {name}: rho32 {rho32:.6e} rho64 {rho64:.6e}; m32 {m32:.9e} m64[9] {mh[9]:.9e} "
               f"m64[10] {mh[10]:.9e} (lag {lag:.3e} of the last iteration); drift {drift:.3e}")
-        record(T, f"{name}: |model lag| (of the 10th iteration's decrease)", abs(lag), LAG_TOL)
+        # the margin log holds non-negative quantities: the behind side as max(lag, 0), the ahead side as max(-lag, 0)
+        record(T, f"{name}: model lag behind (of the 10th iteration's decrease)", max(lag, 0.0), LAG_BEHIND)
+        record(T, f"{name}: model lag ahead (guard)", max(-lag, 0.0), LAG_AHEAD)
         d_rho = record(T, f"{name}: |rho32 - rho64| / rho64 (reported)", abs(rho32 - rho64) / rho64, RHO_GUARD)
         record(T, f"{name}: iterate drift (reported)", drift, DRIFT_GUARD)
-        assert abs(lag) <= LAG_TOL, (name, m32, mh[9], mh[10])
+        assert -LAG_AHEAD <= lag <= LAG_BEHIND, (name, lag, m32, mh[9], mh[10])
         assert rho32 < 1 and d_rho <= RHO_GUARD, (name, rho32, rho64)
         assert drift <= DRIFT_GUARD, (name, drift)
         del prob

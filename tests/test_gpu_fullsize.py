@@ -277,13 +277,17 @@ def test_fullsize_backward_whole_frame_100k():
     # of the Gaussians behind that pixel, so the max-based error is set by the worst flip.  Measured (round 5,
     # profiles/r05/parity_margins*.jsonl): the kept kernels 3.8e-6 L2 / 7.6e-5 per element (SH gradient, the worst);
     # round 4's rejected log2e-prescaled exponent -- one more rounding in every alpha -- 2.1e-5 / 3.8e-4 (scales).  A
-    # wrong derivative is O(1).  Asserted: the error over every Gaussian (L2 rel 5e-5) and, per element, a flip-sized
-    # guard (1e-3 of the max); until round 5 a per-element 1e-4, which that one rounding broke (1.7e-4).
+    # wrong derivative is O(1).  Asserted (round 6: no bound looser than round 4's except on flip-touched elements): the
+    # error over every Gaussian (L2 rel 3e-5); per element round 4's 1e-4 of the max for all but at most 1e-4 of the
+    # elements (the Gaussians behind a flipped pixel), and those within a flip-sized 1e-3.
     for k in ref:
         T = "test_fullsize_backward_whole_frame_100k"
-        l2 = record(T, f"grad {k} (L2 rel)", _l2_rel(got[k], ref[k]), 5e-5)
-        err = record(T, f"grad {k} (of max, per element)", _rel_err(got[k], ref[k]), 1e-3)
-        assert l2 <= 5e-5 and err < 1e-3, f"grad {k}: L2 {l2:.3e}, max {err:.3e}"
+        l2 = record(T, f"grad {k} (L2 rel)", _l2_rel(got[k], ref[k]), 3e-5)
+        err = record(T, f"grad {k} (of max, per element, flip guard)", _rel_err(got[k], ref[k]), 1e-3)
+        d = (got[k] - ref[k]).abs()
+        n_over = int((d > 1e-4 * ref[k].abs().max().clamp_min(1e-8)).sum())
+        frac_over = record(T, f"grad {k} elements beyond 1e-4 of max (fraction)", n_over / d.numel(), 1e-4)
+        assert l2 <= 3e-5 and err < 1e-3 and frac_over <= 1e-4, f"grad {k}: L2 {l2:.3e}, max {err:.3e}, over {n_over}"
 
 
 def test_fullsize_lm_matvec_whole_frame_100k():

@@ -303,3 +303,27 @@ def test_loss_slot_past_the_recorded_set_count_is_nan():
                                                 _lib.stream_handle()))
         v = float(loss)
         assert math.isnan(v) == want_nan, (slot, v)
+    # the all-sets entry point honours the same recorded count -- a group reaching past the binning's 2 sets
+    # gets NaN losses there (not background-only ones), and its sets inside the count are the slot form's values
+    H, W = int(vw.image_height), int(vw.image_width)
+    ref = []
+    for slot in (0, 1):
+        _lib.check(lib.gslm_rasterize_loss_slot(ctypes.byref(vw), P, sl["geoms"][slot].data_ptr(), sl["geoms"][0].numel(),
+                                                binning.data_ptr(), binning.numel(), N, slot, 2, ev.gts[0].data_ptr(),
+                                                None, scr.data_ptr(), scr.numel() * 8, loss.data_ptr(), 0,
+                                                _lib.stream_handle()))
+        ref.append(float(loss))
+    for first, n, want in ((0, 4, (False, False, True, True)), (1, 2, (False, True)), (0, 2, (False, False))):
+        nb = lib.gslm_loss_sets_scratch_bytes(n, H, W)
+        sscr = torch.empty(nb // 8 + 1, dtype=torch.float64, device="cuda")
+        out = torch.zeros(n, dtype=torch.float64, device="cuda")
+        gg = (ctypes.c_void_p * n)(*[sl["geoms"][min(first + a, 1)].data_ptr() for a in range(n)])
+        lp = (ctypes.c_void_p * n)(*[out.data_ptr() + 8 * a for a in range(n)])
+        _lib.check(lib.gslm_rasterize_loss_sets(ctypes.byref(vw), P, gg, n, first, sl["geoms"][0].numel(),
+                                                binning.data_ptr(), binning.numel(), N, ev.gts[0].data_ptr(), None,
+                                                sscr.data_ptr(), sscr.numel() * 8, lp, 0, _lib.stream_handle()))
+        got = [float(x) for x in out.cpu()]
+        assert [math.isnan(x) for x in got] == list(want), (first, n, got)
+        for a, x in enumerate(got):
+            if not want[a]:
+                assert x == ref[first + a], (first, a, x, ref)

@@ -5,8 +5,9 @@ LinearSolverFunctions / GaussianModelState (imported from /root/reference, make_
 the CPU oracle renderer.  Here the same scene runs through libgslm (raw-parameter preprocess,
 fused JVP->VJP matvec, gather-sum backward, device scalars) and must reproduce:
   loss (rel 1e-5), J^T b and (J^T J + D) v (1e-5 of the vector's max), and the CGLS solutions of
-  the reference schedule (max_iter=2, restart_iter=1) and of 10 iterations: the LM model decrease of the step (rel
-  1e-4) and the step itself (rel 1e-4 in norm; 1e-5 for the 2 x 1 schedule until round 5, see CGLS_CASES).
+  the reference schedule (max_iter=2, restart_iter=1) and of 10 iterations: the LM model decrease of the step (one-
+  sided, at most 1e-6 relative less than the reference step's) and the step itself (rel 1e-5 in norm for the 2 x 1
+  schedule, 1e-4 for 10 x 10; see CGLS_CASES).
   The CPU oracle itself reaches 1.6e-7 / 1.3e-6 on the same goldens (tests/test_oracle_golden.py).
 """
 import os
@@ -62,22 +63,27 @@ def test_loss_rhs_matvec_match_reference_solver():
     assert record(T, "(J^T J + D) v (of max)", _err(y.cpu().numpy(), d["Av"]), 1e-5) <= 1e-5
 
 
-def _model_gap(prob, g, x, ref):
-    """|m(x) - m(ref)| / |m(ref)| for the LM model m(v) = 1/2 v^T A v - g^T v on this (GPU) operator: how much less (or
-    more) the step decreases the model than the reference solver's step -- second order in their difference, so
-    stable where the coordinates of an ill-conditioned solve are not."""
+def _model_gap(prob, g, x, ref, signed=False):
+    """(m(x) - m(ref)) / |m(ref)| for the LM model m(v) = 1/2 v^T A v - g^T v on this (GPU) operator (its absolute
+    value unless `signed`): how much less (positive) or more (negative) the step decreases the model than the reference
+    solver's step -- second order in their difference, so stable where the coordinates of an ill-conditioned solve are
+    not."""
     def mval(v):
         av = prob.matvec(v, prob.zeros()).double()
         return float(0.5 * (v.double() * av).sum() - (g.double() * v.double()).sum())
     mr = mval(torch.from_numpy(np.asarray(ref, dtype=np.float32)).cuda())
-    return abs(mval(x) - mr) / abs(mr)
+    d = (mval(x) - mr) / abs(mr)
+    return d if signed else abs(d)
 
 
-# The reference solver's iterates (solver_golden.npz, float32 on the CPU oracle).  Primary: the model decrease of the
-# step (rel 1e-4; round 5 measured ~1e-5).  The coordinates are held to 1e-4 for both schedules: the GPU operator's
-# hardware exp / rcp (DESIGN §5) moves the 2 x 1 iterate by 8.7e-6 of its norm -- against a 1e-5 bound until round 4,
-# which one extra rounding in the exponent broke (1.01e-5, profiles/r04/ab/rec_conic_log2e_rejected/).
-CGLS_CASES = [((2, 1), "x_ref_schedule", 1e-4), ((10, 10), "x_ten", 1e-4)]
+# The reference solver's iterates (solver_golden.npz, float32 on the CPU oracle).  Primary: the LM model decrease of
+# the step, ONE-SIDED (round 6, VERDICT r05 item 4): (m(x) - m(ref)) / |m(ref)| <= MODEL_BEHIND -- the GPU step may
+# decrease the model more than the reference solver's step by any amount, less by at most 1e-6 (worst measured: 5.6e-8
+# in magnitude, 10 x 10); |gap| <= 1e-4 stays as a gross-error guard.  The coordinates are held to round 4's bounds:
+# 1e-5 for the 2 x 1 schedule (measured 8.7e-6 of the norm: the GPU operator's hardware exp / rcp, DESIGN §5) and 1e-4
+# for 10 x 10 (measured 1.6e-5).  Every kernel is deterministic, so these are reproducible run to run.
+CGLS_CASES = [((2, 1), "x_ref_schedule", 1e-5), ((10, 10), "x_ten", 1e-4)]
+MODEL_BEHIND = 1e-6
 
 
 @pytest.mark.parametrize("sched,key,tol", CGLS_CASES)
@@ -91,9 +97,11 @@ def test_cgls_matches_reference_schedule(sched, key, tol):
     ref = d[key]
     err = np.linalg.norm(x.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref)
     T = "test_cgls_matches_reference_schedule"
-    gap = record(T, f"CGLS {sched} model decrease rel", _model_gap(prob, g, x, ref), 1e-4)
+    gap = _model_gap(prob, g, x, ref, signed=True)
+    record(T, f"CGLS {sched} model decrease behind (rel)", max(gap, 0.0), MODEL_BEHIND)
+    record(T, f"CGLS {sched} model decrease |gap| (guard)", abs(gap), 1e-4)
     assert record(T, f"CGLS {sched} iterate rel", err, tol) < tol, err
-    assert gap <= 1e-4, gap
+    assert gap <= MODEL_BEHIND and abs(gap) <= 1e-4, gap
 
 
 def test_cg_nocheck_matches_checked():
@@ -291,15 +299,17 @@ def test_cgls_residual_matches_reference_schedule(sched, key, tol):
     err = np.linalg.norm(x.cpu().numpy().astype(np.float64) - ref) / np.linalg.norm(ref)
     T = "test_cgls_residual_matches_reference_schedule"
     g = prob.rhs(prob.zeros())
-    gap = record(T, f"residual-space CGLS {sched} model decrease rel", _model_gap(prob, g, x, ref), 1e-4)
+    gap = _model_gap(prob, g, x, ref, signed=True)
+    record(T, f"residual-space CGLS {sched} model decrease behind (rel)", max(gap, 0.0), MODEL_BEHIND)
+    record(T, f"residual-space CGLS {sched} model decrease |gap| (guard)", abs(gap), 1e-4)
     assert record(T, f"residual-space CGLS {sched} rel", err, tol) < tol, err
-    assert gap <= 1e-4, gap
+    assert gap <= MODEL_BEHIND and abs(gap) <= 1e-4, gap
 
 
 def test_recursions_against_float64_oracle():
     """10 CGLS iterations of the two float32 recursions (fused normal-equation, residual-space) against the float64
     oracle's CGLS on the golden scene: both decrease the LM model as the float64 step does (rel 1e-5), their
-    coordinates stay within 1e-3 of it (measured 9.2e-5) and within 1e-4 of each other (DESIGN.md reports the
+    coordinates stay within 1e-4 of it (measured 9.2e-5) and within 1e-4 of each other (DESIGN.md reports the
     drift)."""
     import copy
     from gslm.lm import LMProblem, cgls_fused, cgls_residual
@@ -329,14 +339,14 @@ def test_recursions_against_float64_oracle():
     T = "test_recursions_against_float64_oracle"
     # primary: the steps' LM model decrease against the float64 step's (on this operator; second order in their
     # difference); the coordinates against the float64 oracle carry the float32 operator's rounding amplified by 10
-    # iterations (9.2e-5 -- against a 1e-4 bound until round 5), so they keep a 10x guard; the two float32 recursions
-    # on the same operator stay tight
+    # iterations (9.2e-5, the log2e-perturbed build 9.2e-5 too) and are held to round 4's 1e-4 again (round 5 had
+    # widened it to 1e-3); the two float32 recursions on the same operator stay tight
     gf = prob.rhs(prob.zeros())
     x64f = x64.float().cuda()
     mf = record(T, "fused: model decrease rel vs float64", _model_gap(prob, gf, xf, x64f.cpu().numpy()), 1e-5)
     mr = record(T, "residual-space: model decrease rel vs float64", _model_gap(prob, gf, xr, x64f.cpu().numpy()), 1e-5)
-    record(T, "fused vs float64 oracle (coordinates)", ef, 1e-3)
-    record(T, "residual-space vs float64 oracle (coordinates)", er, 1e-3)
+    record(T, "fused vs float64 oracle (coordinates)", ef, 1e-4)
+    record(T, "residual-space vs float64 oracle (coordinates)", er, 1e-4)
     record(T, "fused vs residual-space", efr, 1e-4)
     assert mf <= 1e-5 and mr <= 1e-5, (mf, mr)
-    assert ef < 1e-3 and er < 1e-3 and efr < 1e-4, (ef, er, efr)
+    assert ef < 1e-4 and er < 1e-4 and efr < 1e-4, (ef, er, efr)
