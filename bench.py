@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--forward-steps", type=int, default=None)
     ap.add_argument("--val-views", type=int, default=50, help="line-search validation views (train_jvp.py:214-216)")
     ap.add_argument("--no-side", action="store_true", help="headline + roofline only (profiling runs)")
+    ap.add_argument("--no-rank-slices", action="store_true",
+                    help="skip the per-rank memory / time slices of configs[3] and configs[4] (N = 1 only)")
     return ap.parse_args()
 
 
@@ -173,7 +175,9 @@ def main():
     del pert
     torch.cuda.empty_cache()
 
+    torch.cuda.reset_peak_memory_stats(device)
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
+    model_bytes = torch.cuda.memory_allocated(device)
     # one view per problem (N = 1): the SH-rest group of the CG vectors is carried as its 3 coordinates in
     # the view's SH-rest span (GSLM_MV_SH_REST_PROJECTED); several views: the full layout
     prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device, sh_projection="auto",
@@ -239,6 +243,16 @@ def main():
     torch.cuda.synchronize()
     barrier()
     t_chk = max_over_ranks(time.perf_counter() - t0)
+    # device memory of the CG solve: the torch allocator's peak since the model was created (model,
+    # the problem's library workspaces -- geometry, binning, image state, scratch per view -- the weights and the CG
+    # vectors); nothing else is resident on this rank
+    loc0 = getattr(prob, "local", prob)
+    peak_mem = {"cg_loop": {"max_allocated_gb": peak_gb(device), "model_gb": model_bytes / 1e9,
+                            "workspace_gb": cuda_tensor_bytes(loc0.views) / 1e9,
+                            "note": "torch.cuda.max_memory_allocated from the model's creation through the timed CG "
+                                    "loops (model, every view's library workspaces, weights, CG vectors); "
+                                    "workspace_gb = the views' gslm workspaces alone"}}
+    del loc0
     cg_checked = {"ms_per_step": 1e3 * t_chk / args.steps, "view_matvec_per_s": n_views * args.steps / t_chk,
                   "iters_before_stop": info_chk["iters"], "stop": info_chk.get("stop"),
                   "note": "the timed K iterations with the reference's stopping tests on the device each iteration "
@@ -355,7 +369,11 @@ def main():
     #   per (tile, Gaussian) entry: JVP pass primal gather 44 + tangent gather 40,
     #   VJP pass primal gather 44 + one gradient row 40 (plain store, replaces the atomic RMW)
     #   per pixel: n_contrib 4 + final_T 4 + weight 12
-    alg_bytes = 168 * N0 + 20 * HW
+    alg_strict = 168 * N0 + 20 * HW
+    # SURVEY 8(d)'s own per-unit figures for the two passes the fused kernel runs (B_jvp's 84 N_dup + 16 HW and B_vjp's
+    # 124 N_dup + 24 HW, whose 2 x 40 B per entry is the atomic read-modify-write the row store replaces): `achieved`
+    # is priced on them as the task prescribes; the stricter 168 N + 20 HW above is kept beside it
+    alg_bytes = 208 * N0 + 40 * HW
     achieved = alg_bytes / (render_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_render_matvec.json")
@@ -431,23 +449,44 @@ def main():
         # ---------------- BASELINE configs[2] / [3] as train_jvp.py runs it, on every rank: one full LM step (loss,
         # J^T b, CGLS with 10 iterations and the reference's stopping tests, the 7-point line search on the
         # reference's 50 validation views), sharded over the ranks; and with the training batch as the validation set
+        torch.cuda.reset_peak_memory_stats(device)
+        resident = torch.cuda.memory_allocated(device)
         lm = time_lm_step(model, cams_all, val_all, bg)
-        lm_tv = time_lm_step(model, cams_all, cams_all, bg, reps=1, with_timing=False)
+        from gslm.lm import _VAL_CACHE
+        ev = _VAL_CACHE.get("last")
+        peak_mem["lm_step"] = {"max_allocated_gb": peak_gb(device), "resident_before_gb": resident / 1e9,
+                               "evaluator_workspace_gb": (cuda_tensor_bytes(ev[1]) / 1e9) if ev else None,
+                               "note": "configs[2] LM step (evaluate, J^T b, CGLS 10 with the stopping tests, the line "
+                                       "search on the validation views): allocator peak over its timed reps; "
+                                       "evaluator_workspace_gb = the validation evaluator kept across LM steps "
+                                       "(its per-view depth orders, union lists and slot workspaces)"}
+        del ev
+        lm_tv = time_lm_step(model, cams_all, cams_all, bg, reps=3, with_timing=False)
         # the reference's own CGLS schedule, max_iter = 2, restart_iter = 1 (train_jvp.py:254-256; SURVEY 8(d) config 3
         # "the reference-schedule (2 x 1) variant is also reported")
-        lm_ref = time_lm_step(model, cams_all, val_all, bg, iters=2, restart=1, reps=1)
+        lm_ref = time_lm_step(model, cams_all, val_all, bg, iters=2, restart=1, reps=3)
         # ---------------- BASELINE configs[1]: 100k Gaussians SH 3, one 1080p view, forward + backward
         # through the drop-in autograd surface (GaussianRasterizer, the reference's render() path)
         fb = time_drop_in_fwd_bwd(device, W, H, args.s0, reps=max(args.steps, 5)) if rank == 0 else None
         c0_gpu = time_config0_gpu(device) if rank == 0 else None
         # the drop-in operator at the headline size: what an unchanged train_jvp.py pays per matvec / matvec_T /
         # evaluate_loss (tests/test_jvp_timing.py:71-106 through the reference's call shapes)
+        torch.cuda.reset_peak_memory_stats(device)
+        resident = torch.cuda.memory_allocated(device)
         dropin = time_dropin_solver_ops(model, cams[0], bg) if rank == 0 else None
+        peak_mem["dropin_solver_ops"] = {"max_allocated_gb": peak_gb(device), "resident_before_gb": resident / 1e9,
+                                         "note": "the drop-in J u / J^T v / forward calls through render() at the "
+                                                 "headline size (autograd graphs, dual tensors, rasterizer buffers)"}
         # the SSIM residual (disable_ssim=False): CG iteration on the same view(s)
         ssim = time_ssim_cg(model, cams[:1], bg, steps=args.steps) if world_size == 1 else None
         # first-order path: the fused Adam step at the bench model's size and one train.py
         # iteration (render, L1 + SSIM loss, backward, densification statistics, Adam) at configs[1]'s size
         fo = time_first_order(device, W, H, args.s0, P_adam=args.P, sh=args.sh) if rank == 0 else None
+
+    # ---------------- what one rank of the 8-GPU configs holds, emulated on this GPU (N = 1 only)
+    rank_slices = None
+    if world_size == 1 and not forced and not args.no_side and not args.no_rank_slices:
+        rank_slices = rank_slice_memory(model, cams_all, val_all, bg, device)
 
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
@@ -509,10 +548,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_render_matvec", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": render_ms,
+                         "frac_strict": alg_strict / (render_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "alg_bytes_strict": alg_strict,
                          "frac_visited": alg_visited / (render_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "alg_bytes_visited": alg_visited,
-                         "note": "168 B per list entry + 20 B per pixel; frac_visited counts only the entries "
-                                 "a pixel of their tile can blend (sum over tiles of max n_contrib)"},
+                         "note": "SURVEY 8(d): B_jvp + B_vjp tile terms, (84 + 124) B per list entry + (16 + 24) B "
+                                 "per pixel; frac_strict: 168 B per entry (no atomic RMW: one plain row store) + 20 B "
+                                 "per pixel; frac_visited: the strict model over the entries a pixel of their tile "
+                                 "can blend (sum over tiles of max n_contrib)"},
             "raster_roofline": raster_roofline,
             "tile_stats": ts,
             "cpu_baseline": cpu,
@@ -526,6 +569,7 @@ def main():
             "ssim_cg": ssim,
             "first_order": fo,
             "cg_full_layout": cg_full,
+            "peak_mem": dict(peak_mem, rank_slices=rank_slices),
         }
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
@@ -534,6 +578,105 @@ def main():
         from gslm.parallel import close_native_comms
         close_native_comms()  # (GSLM_COMM=native) every rank at the same point, before the process group goes
         dist.destroy_process_group()
+
+
+def rank_slice_memory(model, cams_all, val_all, bg, device):
+    """Device memory (and time) of one rank's share of the multi-GPU configs, run on this GPU:
+      configs3_lm_step   BASELINE configs[3] at 8 ranks: the LM step of one rank -- its one 1080p training view and its
+                         ceil(50 / 8) = 7 validation views, 1M Gaussians (the model replicated; at one rank the CG
+                         vectors are full-P, an upper bound of the sharded rank's P / 8 slices);
+      configs4_cg_slice  BASELINE configs[4] at 8 ranks: rank 0's CG iterations of the Gaussian-sharded product over
+                         its 4 of 32 4K views, 5M Gaussians (GaussianShardedOperator(emulate=(0, 8)): the collectives
+                         replaced by same-shape local copies)."""
+    from gslm.cameras import orbit_cameras
+    from gslm.lm import LMProblem, cgls_fused, clear_val_cache, lm_step
+    from gslm.model import synthetic_gaussians
+    from gslm.parallel import GaussianShardedOperator
+    out = {}
+    clear_val_cache()
+    torch.cuda.empty_cache()
+    if val_all:
+        saved = [t.detach().clone() for t in model.params()]
+        torch.cuda.reset_peak_memory_stats(device)
+        res = torch.cuda.memory_allocated(device)
+        n_val = -(-len(val_all) // 8)
+        t0 = time.perf_counter()
+        o = lm_step(model, [cams_all[0]], val_all[:n_val], bg, max_iter=10, restart_iter=10)
+        torch.cuda.synchronize()
+        t_lm = time.perf_counter() - t0  # (one step, cold: workspaces allocated inside)
+        with torch.no_grad():
+            for t, s0 in zip(model.params(), saved):
+                if t is not model._xyz:
+                    t.copy_(s0)
+        out["configs3_lm_step"] = {"max_allocated_gb": peak_gb(device), "resident_before_gb": res / 1e9,
+                                   "train_views": 1, "val_views": n_val, "P": int(model._xyz.shape[0]),
+                                   "first_step_ms": 1e3 * t_lm, "best_alpha": o["best_alpha"]}
+        del saved, o
+        clear_val_cache()
+        torch.cuda.empty_cache()
+    P5, W4, H4, per, n = 5_000_000, 3840, 2160, 4, 8
+    torch.cuda.reset_peak_memory_stats(device)
+    res = torch.cuda.memory_allocated(device)
+    cams = [c.to(device) for c in orbit_cameras(n * per, W4, H4, seed=1)]
+    m5 = synthetic_gaussians(P5, 3, seed=0, s0=0.005, device="cpu", n_cams=n * per).to(device)
+    mine = cams[:per]
+    g5 = torch.Generator().manual_seed(7)
+    for c in mine:
+        c.original_image = torch.rand(3, H4, W4, generator=g5).to(device)
+    local = LMProblem(m5, mine, bg, device=device, sh_projection=False)
+    local.evaluate()
+    op = GaussianShardedOperator(local, all_cams=cams, emulate=(0, n))
+    gs = op.rhs(op.zeros())
+    cgls_fused(op, gs, max_iter=2, restart_iter=2, check_every=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    cgls_fused(op, gs, max_iter=3, restart_iter=3, check_every=False)
+    torch.cuda.synchronize()
+    t_it = (time.perf_counter() - t0) / 3
+    out["configs4_cg_slice"] = {"max_allocated_gb": peak_gb(device), "resident_before_gb": res / 1e9, "P": P5,
+                                "views_on_rank": per, "ranks": n, "width": W4, "height": H4,
+                                "workspace_gb": cuda_tensor_bytes(local.views) / 1e9,
+                                "num_rendered": [vr.N for vr in local.views],
+                                "emulated_cg_ms_per_iteration": 1e3 * t_it,
+                                "note": "rank 0 of 8, collectives as local copies (compute only)"}
+    del op, local, gs, m5, cams, mine
+    torch.cuda.empty_cache()
+    return out
+
+
+def cuda_tensor_bytes(*objs, depth=3):
+    """Bytes of the distinct CUDA tensors reachable from objs through attributes, lists, tuples and dicts (depth-
+    limited): the library workspaces a ViewRaster / LossEvaluator holds (geometry, binning, image state, scratch)."""
+    seen, total = set(), 0
+
+    def walk(o, d):
+        nonlocal total
+        if isinstance(o, torch.Tensor):
+            if o.is_cuda:
+                st = o.untyped_storage()
+                if st.data_ptr() not in seen:
+                    seen.add(st.data_ptr())
+                    total += st.nbytes()
+            return
+        if d <= 0:
+            return
+        if isinstance(o, (list, tuple)):
+            for x in o:
+                walk(x, d - 1)
+        elif isinstance(o, dict):
+            for x in o.values():
+                walk(x, d - 1)
+        elif hasattr(o, "__dict__") and not isinstance(o, type):
+            for x in vars(o).values():
+                walk(x, d - 1)
+
+    for o in objs:
+        walk(o, depth)
+    return total
+
+
+def peak_gb(device):
+    return torch.cuda.max_memory_allocated(device) / 1e9
 
 
 def tile_stats(vr, P):
@@ -673,12 +816,13 @@ def time_ssim_cg(model, cams, bg, steps=10):
             "ms_per_step": 1e3 * t, "view_matvec_per_s": len(cams) / t}
 
 
-def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True, restart=None):
+def time_lm_step(model, cams, val_cams, bg, iters=10, reps=5, with_timing=True, restart=None):
     """gslm.lm.lm_step (train_jvp.py:221-289) with max_iter = iters, restart_iter = restart (default iters) and the
     reference's stopping
     tests (on the device), the line search over `val_cams`; every rank calls it (the training and validation views
     are sharded over the ranks inside).  The model is restored after each step, so every rep solves the same
-    problem; the phase breakdown (evaluate + J^T b, CG, line search) comes from one more step with timing=True."""
+    problem.  `ms` is the median of `reps` individually synchronised steps (max over ranks per rep), with the spread
+    beside it; the phase breakdown (evaluate + J^T b, CG, line search) comes from one more step with timing=True."""
     from gslm.lm import lm_step
     saved = [t.detach().clone() for t in model.params()]
 
@@ -696,21 +840,27 @@ def time_lm_step(model, cams, val_cams, bg, iters=10, reps=2, with_timing=True, 
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         out = lm_step(model, cams, val_cams, bg, max_iter=iters, restart_iter=restart)
-        restore()
-    torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / reps
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+        restore()  # (outside the timed region: bench bookkeeping, not part of train_jvp.py's step)
+        torch.cuda.synchronize()
     if dist.is_initialized():
-        tt = torch.tensor([t], dtype=torch.float64, device=saved[0].device)
+        tt = torch.tensor(ts, dtype=torch.float64, device=saved[0].device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+        ts = tt.tolist()
+    srt = sorted(ts)
+    t = srt[len(srt) // 2] if len(srt) % 2 else 0.5 * (srt[len(srt) // 2 - 1] + srt[len(srt) // 2])
     sched = f"{iters} iterations" if restart == iters else f"max_iter {iters} x restart_iter {restart} (the reference's schedule)"
     res = {"config": f"full LM step, {len(cams)} training view(s) over {out['ranks']} rank(s), CGLS {sched} "
                      f"with the reference's stopping tests + 7-point line search on {len(val_cams)} validation "
                      "view(s) (train_jvp.py:237-279; BASELINE configs[2], configs[3] at 8 GPUs)",
-           "ms": 1e3 * t, "cg_iters": out["cg"]["iters"], "val_views": len(val_cams), "ranks": out["ranks"],
+           "ms": 1e3 * t, "reps": reps, "ms_min": 1e3 * srt[0], "ms_max": 1e3 * srt[-1],
+           "ms_mean": 1e3 * sum(srt) / len(srt),
+           "cg_iters": out["cg"]["iters"], "val_views": len(val_cams), "ranks": out["ranks"],
            "val_renders_per_rank": 7 * -(-len(val_cams) // out["ranks"]),
            "loss_start": out["start_loss"], "loss_final": out["final_val_loss"], "best_alpha": out["best_alpha"],
            "line_search": out["line_search"]}
