@@ -35,7 +35,7 @@ extern "C" int gslm_selftest_scan(const uint32_t* in, uint32_t* out, int64_t n, 
     return GSLM_ERR_INVALID;
   }
   if (tmp_bytes < gslm::scan_tmp_bytes(n)) {
-    gslm::set_error("selftest_scan: tmp below 8 ceil(n / 2048) + 64 bytes");
+    gslm::set_error("selftest_scan: tmp below 8 ceil(n / 2048) + 64 bytes rounded up to 256");
     return GSLM_ERR_CAPACITY;
   }
   return gslm::exclusive_scan_u32(in, nullptr, out, n, static_cast<uint32_t*>(tmp), total, (hipStream_t)stream,

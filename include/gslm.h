@@ -559,7 +559,8 @@ int gslm_inspect(const void* geom, int64_t P, const void* binning, int64_t num_r
 int gslm_selftest(int32_t which, const float* in, float* out, void* stream);
 /* Device self-test of the library's exclusive u32 scan (the tile-count and LM row-map scans): out[i] = sum_{j<i} in[j],
  * *total = the sum (both device).  force_top != 0 takes the long-scan form (a scan of the block sums in a launch of
- * its own, used above 4096 blocks of 2048) at any n.  tmp: >= 8 ceil(n / 2048) + 64 bytes of device scratch. */
+ * its own, used above 4096 blocks of 2048) at any n.  tmp: >= 8 ceil(n / 2048) + 64 bytes of device scratch, rounded
+ * up to a multiple of 256. */
 int gslm_selftest_scan(const uint32_t* in, uint32_t* out, int64_t n, int32_t force_top, void* tmp, size_t tmp_bytes,
                        uint32_t* total, void* stream);
 

@@ -43,7 +43,7 @@ def test_exclusive_scan_both_forms(n, force_top):
     x = torch.randint(0, 64, (n,), generator=g, dtype=torch.int64)
     xin = x.to(torch.int32).cuda()
     out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-    tmp = torch.empty(8 * ((n + 2047) // 2048) + 64, dtype=torch.uint8, device="cuda")
+    tmp = torch.empty((8 * ((n + 2047) // 2048) + 64 + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
     tot = torch.zeros(1, dtype=torch.int32, device="cuda")
     _lib.check(_lib.lib.gslm_selftest_scan(xin.data_ptr(), out.data_ptr(), n, force_top, tmp.data_ptr(), tmp.numel(),
                                            tot.data_ptr(), _lib.stream_handle()))
