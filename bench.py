@@ -177,7 +177,7 @@ def main():
 
     torch.cuda.reset_peak_memory_stats(device)
     model = synthetic_gaussians(args.P, args.sh, seed=0, s0=args.s0, device="cpu", n_cams=n_views).to(device)
-    model_bytes = torch.cuda.memory_allocated(device)
+    resident0 = torch.cuda.memory_allocated(device)  # the model + the GT images of the training / validation views
     # one view per problem (N = 1): the SH-rest group of the CG vectors is carried as its 3 coordinates in
     # the view's SH-rest span (GSLM_MV_SH_REST_PROJECTED); several views: the full layout
     prob = ShardedLMProblem(model, cams, bg, all_cams=cams_all, device=device, sh_projection="auto",
@@ -247,11 +247,12 @@ def main():
     # the problem's library workspaces -- geometry, binning, image state, scratch per view -- the weights and the CG
     # vectors); nothing else is resident on this rank
     loc0 = getattr(prob, "local", prob)
-    peak_mem = {"cg_loop": {"max_allocated_gb": peak_gb(device), "model_gb": model_bytes / 1e9,
+    peak_mem = {"cg_loop": {"max_allocated_gb": peak_gb(device), "resident_before_gb": resident0 / 1e9,
                             "workspace_gb": cuda_tensor_bytes(loc0.views) / 1e9,
                             "note": "torch.cuda.max_memory_allocated from the model's creation through the timed CG "
                                     "loops (model, every view's library workspaces, weights, CG vectors); "
-                                    "workspace_gb = the views' gslm workspaces alone"}}
+                                    "resident_before_gb = the model and the GT images of the training and validation "
+                                    "views; workspace_gb = the views' gslm workspaces alone"}}
     del loc0
     cg_checked = {"ms_per_step": 1e3 * t_chk / args.steps, "view_matvec_per_s": n_views * args.steps / t_chk,
                   "iters_before_stop": info_chk["iters"], "stop": info_chk.get("stop"),
