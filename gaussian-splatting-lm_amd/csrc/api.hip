@@ -45,7 +45,7 @@ size_t geom_layout(int64_t P, void* base, GeomBufs* o) {
   g.vals_alt = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.goff = c.take<uint32_t>(P);
-  g.hist = c.take<uint32_t>(std::max(sort_hist_bytes(P), d11_hist_bytes(P)) / 4);  // depth sort (d11) or 8-bit users
+  g.hist = c.take<uint32_t>(sort_hist_bytes(P) / 4);
   g.scan_tmp = c.take<uint32_t>(scan_tmp_bytes(P) / 4);
   g.counters = c.take<uint32_t>(16);
   g.clampw = c.take<uint32_t>(P);
@@ -161,11 +161,15 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
   if (order_mode == 2) {
     GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
   } else {
-    // depth sort of (key, index) pairs, 3 passes of 11-bit digits: the first scatter generates the indices (no iota
-    // pass), the last writes tiles[index] where the sorted keys would go (into keys_alt); the order lands in sorted_idx
-    st = radix_sort_depth(gb.depth_key, gb.keys_alt, gb.sorted_idx, gb.vals_alt, P, gb.hist, gb.tiles, s);
+    // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass), the last writes
+    // tiles[index] where the sorted keys would go.  (Round 6 measured 3 passes of 11-bit digits against these 4 of 8
+    // bits: 90.9 against 90.8 us per 1M keys -- the 2048-digit scatter and scan cost what the fourth pass did --
+    // profiles/r06/ab_depth_sort_d11_neutral/.)
+    bool alt = false;
+    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true, gb.tiles);
     if (st) return st;
-    tiles_sorted = gb.keys_alt;
+    if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
+    tiles_sorted = alt ? gb.keys_alt : gb.depth_key;
     if (order_mode == 1)
       GSLM_HIP_CHECK(hipMemcpyAsync(depth_order, gb.sorted_idx, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
   }

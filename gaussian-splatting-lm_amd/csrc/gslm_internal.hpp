@@ -85,15 +85,6 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
                      const uint32_t* last_gather = nullptr, const uint32_t* n_dev = nullptr, uint32_t* p0 = nullptr,
                      uint32_t* p1 = nullptr);
 
-// The depth sort (sort.hip, k_d11_*): stable LSD sort of n 32-bit keys in 3 passes of 11 + 11 + 10 bits, the values
-// the input indices.  keys / keys_alt and vals_out / vals_alt ping-pong so that the result ends in vals_out (the depth
-// order) and keys_alt (last_gather[value] in sorted order, or the sorted keys when last_gather is NULL).
-// hist: d11_hist_bytes(n).
-inline int64_t d11_blocks(int64_t n) { return (n + 4095) / 4096; }
-inline size_t d11_hist_bytes(int64_t n) { return ((size_t)2048 * (size_t)d11_blocks(n) + 2048) * 4; }
-int radix_sort_depth(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals_out, uint32_t* vals_alt, int64_t n,
-                     uint32_t* hist, const uint32_t* last_gather, hipStream_t s);
-
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;
 #ifndef GSLM_SCAN_ITEMS

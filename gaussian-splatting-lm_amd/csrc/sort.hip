@@ -251,214 +251,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 }
 
-// ---------------- the depth sort: 3 passes of 11-bit digits (11 + 11 + 10 = all 32 key bits) ----------------
-// The depth keys (float bits of the view depth, 0xFFFFFFFF behind the near plane) are sorted on every forward; with
-// 8-bit digits that took 4 passes of 3 dependent launches each, every launch near its ~5 us floor at P = 1M.  2048
-// digits per pass make it 3 passes (exact on every key: no bits are dropped).  4096 keys per block (512 threads, 8 waves
-// of 512 consecutive keys): per-block digit counts in [block][digit] rows (coalesced 16-B stores), scanned over the
-// blocks per digit by k_d11_scan, the digit totals scanned by each scatter block.  Stability as in k_radix_scatter:
-// block order, then wave, round and lane order = input order.
-constexpr int D11_BITS = 11;
-constexpr int D11_RADIX = 1 << D11_BITS;
-constexpr int D11_THREADS = 512;
-constexpr int D11_ITEMS = 8;
-constexpr int D11_TILE = D11_THREADS * D11_ITEMS;  // 4096
-constexpr int D11_DPT = D11_RADIX / D11_THREADS;   // 4 digits per thread
-static_assert(D11_DPT == 4, "uint4 digit rows");
-
-template <int NW>
-__device__ __forceinline__ uint32_t block_incl_scan_nw(uint32_t x, uint32_t* s_w, uint32_t* total) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t inc = wave_incl_scan(x, lane);
-  if (lane == 63) s_w[w] = inc;
-  __syncthreads();
-  uint32_t off = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < NW; ++k) {
-    const uint32_t v = s_w[k];
-    if (k < w) off += v;
-    tot += v;
-  }
-  __syncthreads();
-  *total = tot;
-  return inc + off;
-}
-
-__global__ __launch_bounds__(D11_THREADS) void k_d11_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                          uint32_t dmask, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t cnt[D11_RADIX];
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < D11_DPT; ++k) cnt[tid + k * D11_THREADS] = 0u;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * D11_TILE;
-#pragma unroll
-  for (int r = 0; r < D11_ITEMS; ++r) {
-    const int64_t i = base + r * D11_THREADS + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
-  }
-  __syncthreads();
-  reinterpret_cast<uint4*>(hist + (int64_t)blockIdx.x * D11_RADIX)[tid] =
-      make_uint4(cnt[4 * tid], cnt[4 * tid + 1], cnt[4 * tid + 2], cnt[4 * tid + 3]);
-}
-
-// Block j: digits 8j .. 8j + 7.  Per digit the exclusive scan of its count over the nb blocks (in place, [block][digit]
-// rows) and the digit's total (totals[d], unscanned).
-__global__ __launch_bounds__(256) void k_d11_scan(uint32_t* __restrict__ hist, int nb, uint32_t* __restrict__ totals) {
-  __shared__ uint32_t s_w[4][8];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int d0 = 8 * blockIdx.x;
-  uint32_t carry[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) carry[k] = 0u;
-  for (int c = 0; c < nb; c += 256) {
-    const int b = c + tid;
-    uint4 lo = make_uint4(0u, 0u, 0u, 0u), hi = lo;
-    uint4* row = reinterpret_cast<uint4*>(hist + (int64_t)b * D11_RADIX + d0);
-    if (b < nb) {
-      lo = row[0];
-      hi = row[1];
-    }
-    uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    uint32_t inc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      inc[k] = wave_incl_scan(x[k], lane);
-      if (lane == 63) s_w[w][k] = inc[k];
-    }
-    __syncthreads();
-    uint32_t ex[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      uint32_t off = 0, tot = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t v = s_w[q][k];
-        if (q < w) off += v;
-        tot += v;
-      }
-      ex[k] = carry[k] + off + inc[k] - x[k];
-      carry[k] += tot;
-    }
-    __syncthreads();
-    if (b < nb) {
-      row[0] = make_uint4(ex[0], ex[1], ex[2], ex[3]);
-      row[1] = make_uint4(ex[4], ex[5], ex[6], ex[7]);
-    }
-  }
-  if (tid == 0) {
-    reinterpret_cast<uint4*>(totals + d0)[0] = make_uint4(carry[0], carry[1], carry[2], carry[3]);
-    reinterpret_cast<uint4*>(totals + d0)[1] = make_uint4(carry[4], carry[5], carry[6], carry[7]);
-  }
-}
-
-// vin == NULL: the values are the indices (the first pass); kgather (the last pass): kgather[value] is written where
-// the sorted key would go (the tile counts in depth order)
-__global__ __launch_bounds__(D11_THREADS) void k_d11_scatter(const uint32_t* __restrict__ kin,
-                                                             const uint32_t* __restrict__ vin,
-                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                             int64_t n, int shift, int nbits,
-                                                             const uint32_t* __restrict__ hist,
-                                                             const uint32_t* __restrict__ totals,
-                                                             const uint32_t* __restrict__ kgather) {
-  constexpr int NW = D11_THREADS / 64;
-  constexpr int WAVE_KEYS = D11_TILE / NW;  // 512: 8 rounds of 64
-  __shared__ uint32_t s_keys[D11_TILE], s_vals[D11_TILE];
-  __shared__ uint32_t s_wcnt[NW][D11_RADIX];  // per-wave running digit count, then the wave's offset in the digit's run
-  __shared__ uint32_t s_loc[D11_RADIX];       // block-local start of each digit's run
-  __shared__ uint32_t s_gbase[D11_RADIX];     // global offset of this block's run of each digit
-  __shared__ uint32_t s_w[NW];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * D11_TILE;
-  const int nvalid = (int)min<int64_t>(D11_TILE, n - base);
-  const int wbase = w * WAVE_KEYS;
-  const uint32_t dmask = (1u << nbits) - 1u;
-  for (int k = lane; k < D11_RADIX; k += 64) s_wcnt[w][k] = 0u;
-  wave_order_lds();
-  uint32_t key[D11_ITEMS], val[D11_ITEMS], lrank[D11_ITEMS];
-#pragma unroll
-  for (int r = 0; r < D11_ITEMS; ++r) {
-    const int64_t i = base + wbase + r * 64 + lane;
-    key[r] = i < n ? kin[i] : 0u;
-    val[r] = i < n ? (vin ? vin[i] : (uint32_t)i) : 0u;
-  }
-  {
-    // global base of each digit's run: exclusive prefix of the digit totals + this block's exclusive prefix (k_d11_scan)
-    const uint4 t = reinterpret_cast<const uint4*>(totals)[tid];
-    const uint4 h = reinterpret_cast<const uint4*>(hist + (int64_t)blockIdx.x * D11_RADIX)[tid];
-    const uint32_t sum = (t.x + t.y) + (t.z + t.w);
-    uint32_t tot;
-    const uint32_t ex = block_incl_scan_nw<NW>(sum, s_w, &tot) - sum;
-    s_gbase[4 * tid] = ex + h.x;
-    s_gbase[4 * tid + 1] = ex + t.x + h.y;
-    s_gbase[4 * tid + 2] = ex + t.x + t.y + h.z;
-    s_gbase[4 * tid + 3] = ex + t.x + t.y + t.z + h.w;
-  }
-  // 1. wave-local stable rank of every key among equal digits
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-#pragma unroll
-  for (int r = 0; r < D11_ITEMS; ++r) {
-    const bool valid = wbase + r * 64 + lane < nvalid;
-    const uint32_t d = (key[r] >> shift) & dmask;
-    unsigned long long m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < D11_BITS; ++b) {  // (bits at or above nbits are 0 in every lane's d: m unchanged)
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
-    }
-    const uint32_t rank = __popcll(m & lt_mask);
-    const uint32_t cnt = s_wcnt[w][d];
-    lrank[r] = cnt + rank;
-    if (valid && rank == 0) s_wcnt[w][d] = cnt + (uint32_t)__popcll(m);
-    wave_order_lds();
-  }
-  __syncthreads();
-  // 2. the waves' offsets inside each digit's run, and each run's block-local start (4 digits per thread)
-  {
-    uint32_t c[D11_DPT];
-#pragma unroll
-    for (int k = 0; k < D11_DPT; ++k) {
-      const int d = 4 * tid + k;
-      uint32_t run = 0;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const uint32_t v = s_wcnt[q][d];
-        s_wcnt[q][d] = run;
-        run += v;
-      }
-      c[k] = run;
-    }
-    const uint32_t sum = (c[0] + c[1]) + (c[2] + c[3]);
-    uint32_t tot;
-    const uint32_t ex = block_incl_scan_nw<NW>(sum, s_w, &tot) - sum;
-    s_loc[4 * tid] = ex;
-    s_loc[4 * tid + 1] = ex + c[0];
-    s_loc[4 * tid + 2] = ex + c[0] + c[1];
-    s_loc[4 * tid + 3] = ex + c[0] + c[1] + c[2];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < D11_ITEMS; ++r) {
-    if (wbase + r * 64 + lane < nvalid) {
-      const uint32_t d = (key[r] >> shift) & dmask;
-      const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
-      s_keys[lp] = key[r];
-      s_vals[lp] = val[r];
-    }
-  }
-  __syncthreads();
-  // 3. each run to its global offset, consecutive threads on consecutive elements
-  for (int e = tid; e < nvalid; e += D11_THREADS) {
-    const uint32_t k = s_keys[e];
-    const uint32_t d = (k >> shift) & dmask;
-    const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_loc[d]);
-    const uint32_t v = s_vals[e];
-    kout[pos] = kgather ? kgather[v] : k;
-    vout[pos] = v;
-  }
-}
-
 // ---------------- scan ----------------
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint32_t* __restrict__ in,
                                                               const uint32_t* __restrict__ idx, int64_t n,
@@ -676,29 +468,6 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
     alt = !alt;
   }
   *result_in_alt = alt;
-  return GSLM_OK;
-}
-
-int radix_sort_depth(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals_out, uint32_t* vals_alt, int64_t n,
-                     uint32_t* hist, const uint32_t* last_gather, hipStream_t s) {
-  if (n <= 0) return GSLM_OK;
-  const int nb = (int)d11_blocks(n);
-  uint32_t* totals = hist + (size_t)D11_RADIX * nb;
-  // pass 1: keys -> keys_alt, iota -> vals_out; pass 2: keys_alt -> keys, vals_out -> vals_alt; pass 3: keys ->
-  // keys_alt (last_gather[value]), vals_alt -> vals_out
-  const uint32_t* ki[3] = {keys, keys_alt, keys};
-  uint32_t* ko[3] = {keys_alt, keys, keys_alt};
-  const uint32_t* vi[3] = {nullptr, vals_out, vals_alt};
-  uint32_t* vo[3] = {vals_out, vals_alt, vals_out};
-  const int shifts[3] = {0, 11, 22}, bits[3] = {11, 11, 10};
-  for (int p = 0; p < 3; ++p) {
-    const uint32_t dmask = (1u << bits[p]) - 1u;
-    hipLaunchKernelGGL(k_d11_hist, dim3(nb), dim3(D11_THREADS), 0, s, ki[p], n, shifts[p], dmask, hist);
-    hipLaunchKernelGGL(k_d11_scan, dim3(D11_RADIX / 8), dim3(256), 0, s, hist, nb, totals);
-    hipLaunchKernelGGL(k_d11_scatter, dim3(nb), dim3(D11_THREADS), 0, s, ki[p], vi[p], ko[p], vo[p], n, shifts[p],
-                       bits[p], (const uint32_t*)hist, (const uint32_t*)totals, p == 2 ? last_gather : nullptr);
-    GSLM_LAUNCH_CHECK();
-  }
   return GSLM_OK;
 }
 
