@@ -682,7 +682,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     # Same arithmetic, the same iterates bitwise (round 6).
     side_mode = defer and getattr(prob, "supports_xpby_side", False) and os.environ.get("GSLM_CG_SIDE_X", "1") != "0"
     side = torch.cuda.Stream(dev) if side_mode else None
-    p_spare = torch.empty_like(x) if side_mode else None
+    # (zeroed: with mask_xyz no update writes the xyz group, which must read as the zeros of every LM iterate)
+    p_spare = torch.zeros_like(x) if side_mode else None
     SNAP = (8, 9)  # alpha snapshots, by iteration parity
     n_side = 0
     # Gaussian-sharded operators (gslm.parallel.GaussianShardedOperator) hold a shard of every vector: each
