@@ -318,8 +318,15 @@ class LMProblem:
         safe to read or overwrite)."""
         ev = getattr(self, "_x_evt", None)
         if ev is not None:
-            torch.cuda.ExternalStream(self.stream).wait_event(ev)
+            self._main_stream().wait_event(ev)
             self._x_evt = None
+
+    def _main_stream(self):
+        """The torch stream object of self.stream (the current stream the problem was built on)."""
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != self.stream:
+            raise RuntimeError("gslm: the current stream changed since the LMProblem was built")
+        return cur
 
     def matvec_dot(self, v, y, dot_out, pre=None, exposure_zero=False, cg_ctl=None):
         """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
@@ -433,7 +440,7 @@ class LMProblem:
         if pre.get("anum") is not None:
             side, lo, x = pre["side"], pre["lo"], pre["x"]
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.ExternalStream(self.stream))
+            ev.record(self._main_stream())
             side.wait_event(ev)
             n = x.numel() - lo
             check(lib.gslm_axpy_dev(n, pre["snap"], None, 1.0, p_in.data_ptr() + 4 * lo, x.data_ptr() + 4 * lo,
@@ -681,7 +688,8 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     # of streaming x through the tangent kernel (alpha stored per iteration parity, gslm_matvec_opts.alpha_snap).
     # Same arithmetic, the same iterates bitwise (round 6).
     side_mode = defer and getattr(prob, "supports_xpby_side", False) and os.environ.get("GSLM_CG_SIDE_X", "1") != "0"
-    side = torch.cuda.Stream(dev) if side_mode else None
+    side = (torch.cuda.current_stream(dev) if os.environ.get("GSLM_CG_SIDE_SAME") == "1" else torch.cuda.Stream(dev)) \
+        if side_mode else None
     # (zeroed: with mask_xyz no update writes the xyz group, which must read as the zeros of every LM iterate)
     p_spare = torch.zeros_like(x) if side_mode else None
     SNAP = (8, 9)  # alpha snapshots, by iteration parity
