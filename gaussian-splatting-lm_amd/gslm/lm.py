@@ -438,14 +438,15 @@ class LMProblem:
                                       vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o1), self.stream),
               "gslm_matvec_view_ex (tangent)")
         if pre.get("anum") is not None:
+            # (the events and the main stream's torch object come with pre: created once per solve, not per product)
             side, lo, x = pre["side"], pre["lo"], pre["x"]
-            ev = torch.cuda.Event()
-            ev.record(self._main_stream())
+            ev = pre["ev_t"]
+            ev.record(pre["main"])
             side.wait_event(ev)
             n = x.numel() - lo
             check(lib.gslm_axpy_dev(n, pre["snap"], None, 1.0, p_in.data_ptr() + 4 * lo, x.data_ptr() + 4 * lo,
                                     side.cuda_stream), "gslm_axpy_dev (side)")
-            self._x_evt = torch.cuda.Event()
+            self._x_evt = pre["ev_x"]
             self._x_evt.record(side)
 
     def _pre_without_views(self, v, pre):
@@ -690,6 +691,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     side_mode = defer and getattr(prob, "supports_xpby_side", False) and os.environ.get("GSLM_CG_SIDE_X", "1") != "0"
     side = (torch.cuda.current_stream(dev) if os.environ.get("GSLM_CG_SIDE_SAME") == "1" else torch.cuda.Stream(dev)) \
         if side_mode else None
+    side_ev = (prob._main_stream(), torch.cuda.Event(), torch.cuda.Event()) if side_mode else None
     # (zeroed: with mask_xyz no update writes the xyz group, which must read as the zeros of every LM iterate)
     p_spare = torch.zeros_like(x) if side_mode else None
     SNAP = (8, 9)  # alpha snapshots, by iteration parity
@@ -734,7 +736,7 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
                 # p_new = s + beta p (out of place), x += alpha_prev p on the side stream
                 full = {"s": pre[0], "num": pre[1], "den": pre[2], "p_in": p, "x": x, "lo": lo, "side": side,
                         "anum": pend[0] if pend is not None else None, "aden": pend[1] if pend is not None else None,
-                        "snap": ptr(SNAP[n_side & 1])}
+                        "snap": ptr(SNAP[n_side & 1]), "main": side_ev[0], "ev_t": side_ev[1], "ev_x": side_ev[2]}
                 n_side += 1
                 pend = None
                 p, p_spare = p_spare, p
