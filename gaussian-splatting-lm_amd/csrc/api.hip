@@ -700,16 +700,6 @@ static int build_xpby(const gslm_matvec_opts* opts, const gslm_grads* vin, int R
     set_error("matvec: deferred x update needs alpha_den and a float-aligned xpby_x_offset");
     return GSLM_ERR_INVALID;
   }
-  xp.pin = opts->xpby_in_offset / (int64_t)sizeof(float);
-  xp.alpha_snap = opts->alpha_snap;
-  if (opts->xpby_in_offset % (int64_t)sizeof(float) != 0) {
-    set_error("matvec: xpby_in_offset must be float-aligned");
-    return GSLM_ERR_INVALID;
-  }
-  if (xp.alpha_snap && !xp.anum) {
-    set_error("matvec: alpha_snap needs alpha_num / alpha_den");
-    return GSLM_ERR_INVALID;
-  }
   *out = xp;
   return GSLM_OK;
 }

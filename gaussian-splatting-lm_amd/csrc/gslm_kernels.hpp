@@ -566,10 +566,6 @@ struct XpbyK {
   const double* anum;
   const double* aden;
   int64_t xoff;
-  // ABI 10: the previous direction at p + pin floats (0: in place), the update written to p; alpha_snap (or NULL):
-  // with anum set, *alpha_snap = anum / aden is stored (block 0) instead of the x update (the caller applies it)
-  int64_t pin;
-  double* alpha_snap;
 };
 // compact: the LM rows' 8-float tangent records (store_trec, tangent.hip) instead of 12 floats
 int launch_tangent_pre(const ViewK& v, const GaussK& g, const GaussK& t, const float* m2t, const GeomBufs& gb,

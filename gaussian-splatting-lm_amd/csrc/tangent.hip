@@ -15,14 +15,10 @@ namespace gslm {
 // SH rest when projected: <= 4 floats per Gaussian, so <= 4 elements per thread each) are loaded in one pass --
 // every s / p / x load of the block in flight before the first store -- instead of one latency per group; a
 // full-layout SH rest (3(M-1) floats per Gaussian) streams in its own loop.
-// xp.pin != 0: the previous direction is read from p + pin (left intact) and the update written to p; xp.alpha_snap:
-// alpha is stored for the caller's own x update instead of applying it here.
 __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_rest) {
   const float b = (float)((*xp.num) / (*xp.den));
-  if (xp.anum && xp.alpha_snap && blockIdx.x == 0 && threadIdx.x == 0) *xp.alpha_snap = (*xp.anum) / (*xp.aden);
-  const bool with_x = xp.anum != nullptr && xp.alpha_snap == nullptr;
+  const bool with_x = xp.anum != nullptr;
   const float a = with_x ? (float)((*xp.anum) / (*xp.aden)) : 0.f;  // gslm_cg_update's alpha, bitwise
-  const int64_t pin = xp.pin;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t nv = min((int64_t)blockDim.x, P - i0);
   const int tid = threadIdx.x;
@@ -38,7 +34,7 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
       const bool on = xp.p[k] && (k != 2 || rest_narrow) && e < nv * xp.w[k];
       const int64_t gi = i0 * xp.w[k] + e;
       sv[n] = on ? xp.s[k][gi] : 0.f;
-      pv[n] = on ? xp.p[k][pin + gi] : 0.f;
+      pv[n] = on ? xp.p[k][gi] : 0.f;
       xv[n] = (on && with_x) ? xp.p[k][xp.xoff + gi] : 0.f;
     }
   }
@@ -69,7 +65,7 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
       for (int u = 0; u < U; ++u) {
         const int64_t e = e0 + (int64_t)u * blockDim.x + tid;
         su[u] = e < len ? s[e] : 0.f;
-        pu[u] = e < len ? p[pin + e] : 0.f;
+        pu[u] = e < len ? p[e] : 0.f;
         xu[u] = (e < len && with_x) ? p[xp.xoff + e] : 0.f;
       }
 #pragma unroll
@@ -86,7 +82,7 @@ __device__ __forceinline__ void block_xpby(const XpbyK& xp, int64_t P, float* s_
   }
   if (blockIdx.x == 0 && xp.tail_p)
     for (int64_t e = threadIdx.x; e < xp.tail_n; e += blockDim.x) {
-      const float pvt = xp.tail_p[pin + e];
+      const float pvt = xp.tail_p[e];
       if (with_x) xp.tail_p[xp.xoff + e] = xp.tail_p[xp.xoff + e] + a * pvt;
       xp.tail_p[e] = xp.tail_s[e] + b * pvt;
     }

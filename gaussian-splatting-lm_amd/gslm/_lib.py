@@ -64,7 +64,6 @@ class GslmMatvecOpts(ctypes.Structure):
         ("trec_in", ctypes.c_void_p), ("screen_stride", ctypes.c_int64),
         ("cg_ctl", ctypes.c_void_p),
         ("rest_basis", ctypes.c_void_p), ("rest_views", ctypes.c_int32), ("view_base", ctypes.c_int32),
-        ("xpby_in_offset", ctypes.c_int64), ("alpha_snap", ctypes.c_void_p),
     ]
 
 
@@ -243,7 +242,7 @@ EXPORTS = {
 }
 
 
-ABI_VERSION = 10  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
+ABI_VERSION = 9  # GSLM_ABI_VERSION of include/gslm.h these structs mirror
 
 
 class GslmError(RuntimeError):

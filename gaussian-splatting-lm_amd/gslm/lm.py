@@ -307,27 +307,6 @@ class LMProblem:
     supports_exposure_zero = True
     supports_cg_ctl = True
 
-    @property
-    def supports_xpby_side(self):
-        """cgls_fused's benchmark mode may pass the out-of-place direction update with the x update on a side stream
-        (a dict `pre`, see local_normal_matvec): the disable_ssim product with at least one view."""
-        return not self.ssim and len(self.views) > 0
-
-    def wait_side(self):
-        """Order the problem's stream after the last side-stream x update (x and the previous direction are then
-        safe to read or overwrite)."""
-        ev = getattr(self, "_x_evt", None)
-        if ev is not None:
-            self._main_stream().wait_event(ev)
-            self._x_evt = None
-
-    def _main_stream(self):
-        """The torch stream object of self.stream (the current stream the problem was built on)."""
-        cur = torch.cuda.current_stream(self.device)
-        if cur.cuda_stream != self.stream:
-            raise RuntimeError("gslm: the current stream changed since the LMProblem was built")
-        return cur
-
     def matvec_dot(self, v, y, dot_out, pre=None, exposure_zero=False, cg_ctl=None):
         """matvec, and when possible <v, y> -> device double* dot_out fused into the gather (single
         view; exposure components of v zero, as in every LM iterate).  Returns True if fused.
@@ -365,13 +344,7 @@ class LMProblem:
             opts.flags = (MV_TAIL_CLEAN if vr.tail_clean else 0) | self.mv_flags
             opts.damp7 = self._damps if (damp and b == 0) else None
             opts.cg_ctl = cg_ctl
-            if isinstance(pre, dict) and b == 0:
-                # cgls_fused's benchmark mode: v = s + beta p_prev out of place (p_prev left intact) in the TANGENT
-                # stage alone, alpha of the previous step stored on the device; then x += alpha p_prev on a side
-                # stream beside this product's tile pass, and RENDER | GATHER here
-                self._tangent_side(vr, g, vs, ys, opts, v, pre)
-                opts.stages = 2 | 4 | STAGE_OVERWRITE
-            elif pre is not None and b == 0:
+            if pre is not None and b == 0:
                 ss = self._pre_opts(opts, v, pre)  # noqa: F841  (kept alive for the call)
             if dot_out is not None and b == last:
                 opts.dot_vy = dot_out
@@ -410,44 +383,6 @@ class LMProblem:
             opts.alpha_num, opts.alpha_den = anum, aden
             opts.xpby_x_offset = x.data_ptr() - v.data_ptr()
         return ss
-
-    def _tangent_side(self, vr, g, vs, ys, opts, v, pre):
-        """The TANGENT stage of the first view with the out-of-place direction update v = s + beta p_prev and alpha
-        stored to pre["snap"]; then, on pre["side"] after it, x += alpha p_prev over [lo, n) (gslm_axpy_dev with the
-        stored alpha: the arithmetic of the fused x update, bitwise).  The next product's direction update (which
-        overwrites p_prev's buffer) and any read of x wait for it (wait_side)."""
-        self.wait_side()
-        o1 = _lib.GslmMatvecOpts()
-        o1.stages = 1  # TANGENT
-        o1.flags = opts.flags
-        o1.cg_ctl = opts.cg_ctl
-        s, p_in = pre["s"], pre["p_in"]
-        e0, e1 = self.layout.offsets["exposure"]
-        ss = self.layout.grads_struct(s)
-        o1.xpby_s = ctypes.addressof(ss)
-        o1.beta_num, o1.beta_den = pre["num"], pre["den"]
-        o1.xpby_tail_v = v.data_ptr() + 4 * e0
-        o1.xpby_tail_s = s.data_ptr() + 4 * e0
-        o1.xpby_tail_n = e1 - e0
-        o1.xpby_in_offset = p_in.data_ptr() - v.data_ptr()
-        if pre.get("anum") is not None:
-            o1.alpha_num, o1.alpha_den, o1.alpha_snap = pre["anum"], pre["aden"], pre["snap"]
-        check(lib.gslm_matvec_view_ex(ctypes.byref(vr.view), ctypes.byref(g), ctypes.byref(vs),
-                                      self.weights[0].data_ptr(), int(self.mask_xyz), vr.geom.data_ptr(),
-                                      vr.binning.data_ptr(), vr.N, vr.image.data_ptr(), vr.scratch.data_ptr(),
-                                      vr.scratch.numel(), ctypes.byref(ys), ctypes.byref(o1), self.stream),
-              "gslm_matvec_view_ex (tangent)")
-        if pre.get("anum") is not None:
-            # (the events and the main stream's torch object come with pre: created once per solve, not per product)
-            side, lo, x = pre["side"], pre["lo"], pre["x"]
-            ev = pre["ev_t"]
-            ev.record(pre["main"])
-            side.wait_event(ev)
-            n = x.numel() - lo
-            check(lib.gslm_axpy_dev(n, pre["snap"], None, 1.0, p_in.data_ptr() + 4 * lo, x.data_ptr() + 4 * lo,
-                                    side.cuda_stream), "gslm_axpy_dev (side)")
-            self._x_evt = pre["ev_x"]
-            self._x_evt.record(side)
 
     def _pre_without_views(self, v, pre):
         s, num, den = pre[:3]
@@ -683,19 +618,6 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
     # the update kernel then streams s and q only; the iterates are bitwise those of the undeferred loop.
     defer = not check_every and callback is None
     pend = None  # (alpha_num, alpha_den) of a deferred x update not yet applied
-    # Where the problem supports it (LMProblem.supports_xpby_side), the direction alternates between two buffers
-    # (p = s + beta p_prev written out of place, gslm_matvec_opts.xpby_in_offset) and the deferred x += alpha p_prev
-    # runs on a side stream beside the product's tile pass -- the tile pass is issue-bound, HBM mostly idle -- instead
-    # of streaming x through the tangent kernel (alpha stored per iteration parity, gslm_matvec_opts.alpha_snap).
-    # Same arithmetic, the same iterates bitwise (round 6).
-    side_mode = defer and getattr(prob, "supports_xpby_side", False) and os.environ.get("GSLM_CG_SIDE_X", "1") != "0"
-    side = (torch.cuda.current_stream(dev) if os.environ.get("GSLM_CG_SIDE_SAME") == "1" else torch.cuda.Stream(dev)) \
-        if side_mode else None
-    side_ev = (prob._main_stream(), torch.cuda.Event(), torch.cuda.Event()) if side_mode else None
-    # (zeroed: with mask_xyz no update writes the xyz group, which must read as the zeros of every LM iterate)
-    p_spare = torch.zeros_like(x) if side_mode else None
-    SNAP = (8, 9)  # alpha snapshots, by iteration parity
-    n_side = 0
     # Gaussian-sharded operators (gslm.parallel.GaussianShardedOperator) hold a shard of every vector: each
     # dot / update pass leaves a per-shard partial that is summed over the ranks before it is used
     red = getattr(prob, "allreduce_scalars", None)
@@ -706,8 +628,6 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
 
     def flush():
         nonlocal pend
-        if side_mode:
-            prob.wait_side()  # the side stream's x updates before x is read or updated here
         if pend is not None:
             check(lib.gslm_axpy_dev(na, pend[0], pend[1], 1.0, off(p), off(x), st), "gslm_axpy_dev")
             pend = None
@@ -732,18 +652,9 @@ def cgls_fused(prob, g, max_iter=10, restart_iter=10, tol=1e-10, atol=0.0, check
         for _ in range(restart_iter):
             # [p = s + beta p and the deferred x += alpha p, both fused into this product's tangent kernel]
             # q = A p and delta = <p, A p> (= |J p|^2 + p.D.p), fused into the gather when possible
-            if side_mode and pre is not None:
-                # p_new = s + beta p (out of place), x += alpha_prev p on the side stream
-                full = {"s": pre[0], "num": pre[1], "den": pre[2], "p_in": p, "x": x, "lo": lo, "side": side,
-                        "anum": pend[0] if pend is not None else None, "aden": pend[1] if pend is not None else None,
-                        "snap": ptr(SNAP[n_side & 1]), "main": side_ev[0], "ev_t": side_ev[1], "ev_x": side_ev[2]}
-                n_side += 1
+            full = None if pre is None else pre + ((x, pend[0], pend[1]) if pend is not None else (None, None, None))
+            if full is not None:
                 pend = None
-                p, p_spare = p_spare, p
-            else:
-                full = None if pre is None else pre + ((x, pend[0], pend[1]) if pend is not None else (None, None, None))
-                if full is not None:
-                    pend = None
             # (q was allocated zero; with g's exposure slice zero every iterate's is: J has no exposure column
             # and x0 = 0)
             if not prob.matvec_dot(p, q, ptr(DEL), pre=full, **ez, **ctl_kw):

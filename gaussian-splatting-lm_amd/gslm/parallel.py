@@ -130,12 +130,6 @@ class ShardedOperator:
         the exchanges' products write y themselves."""
         return (not collectives_on(self.world_size)) and getattr(self.local, "supports_exposure_zero", False)
 
-    @property
-    def supports_xpby_side(self):
-        """cgls_fused's side-stream x update (LMProblem.supports_xpby_side): the local problem's products only, i.e.
-        without collectives (the exchanges keep the in-place direction update)."""
-        return (not collectives_on(self.world_size)) and getattr(self.local, "supports_xpby_side", False)
-
     def __init__(self, local, group=None, all_cams=None, exchange="auto"):
         self.local = local
         self.group = group
@@ -286,7 +280,6 @@ class GaussianShardedOperator:
 
     exchange = "gaussian"
     supports_exposure_zero = False  # (not forwarded to the local problem by __getattr__)
-    supports_xpby_side = False  # the shard's direction update stays in place (gslm_tangent_views)
     supports_cg_ctl = True  # cgls_fused's device control block: the tile pass of a stopped solve returns at once
 
     def __init__(self, local, group=None, all_cams=None, emulate=None):

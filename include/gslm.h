@@ -39,7 +39,7 @@ extern "C" {
 #define GSLM_ERR_HIP (-2)
 #define GSLM_ERR_CAPACITY (-3) /* a workspace is too small; the required size is reported */
 
-#define GSLM_ABI_VERSION 10
+#define GSLM_ABI_VERSION 9
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:36-50) as a POD. */
 typedef struct gslm_view {
@@ -324,15 +324,6 @@ typedef struct gslm_matvec_opts {
   const float* rest_basis;
   int32_t rest_views;
   int32_t view_base;
-  /* ABI 10: the direction update out of place, and the x update handed to the caller.  xpby_in_offset (bytes, 0 =
-   * in place): the update reads the previous direction from v + xpby_in_offset (a second flat vector of the same
-   * layout, groups and tail) and writes s + beta p_prev into v, leaving p_prev intact.  alpha_snap (device double,
-   * or NULL): with alpha_num / alpha_den set, the TANGENT stage stores alpha = *alpha_num / *alpha_den there and
-   * does NOT apply the deferred x update -- the caller applies x += alpha p_prev itself (gslm_axpy_dev with
-   * alpha_snap as num and NULL as den, bitwise the same arithmetic), e.g. on a side stream beside the tile pass, where
-   * neither the overwritten scalars nor the next direction can race it.  cgls_fused's benchmark mode uses both. */
-  int64_t xpby_in_offset;
-  double* alpha_snap;
 } gslm_matvec_opts;
 int gslm_matvec_view_ex(const gslm_view* view, const gslm_gaussians* g, const gslm_grads* v,
                         const float* pixel_weight, int32_t mask_xyz, const void* geom, const void* binning,

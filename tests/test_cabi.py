@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_sizes():
     from gslm import _lib
     lib = _lib.lib
-    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 10
+    assert lib.gslm_abi_version() == _lib.ABI_VERSION == 9
     g1, g2 = lib.gslm_geom_bytes(1000), lib.gslm_geom_bytes(2000)
     assert 0 < g1 < g2
     assert lib.gslm_binning_bytes(10_000, 1080, 1920) > 10_000 * 16

@@ -104,24 +104,6 @@ def test_cgls_matches_reference_schedule(sched, key, tol):
     assert gap <= MODEL_BEHIND and abs(gap) <= 1e-4, gap
 
 
-@pytest.mark.parametrize("sched", [(5, 5), (6, 3), (4, 1)])
-def test_cg_side_stream_x_update_is_bitwise(sched, monkeypatch):
-    """Round 6: the benchmark mode's direction in two buffers (gslm_matvec_opts.xpby_in_offset) with x += alpha p on a
-    side stream beside the tile pass (alpha_snap) gives bitwise the iterate of the in-place fused update
-    (GSLM_CG_SIDE_X=0) and of the checked loop, restarts included."""
-    from gslm.lm import LMProblem, cgls_fused
-    d, m, cams = _load()
-    prob = LMProblem(m, cams, torch.zeros(3))
-    prob.evaluate()
-    g = prob.rhs(prob.zeros())
-    x_side, _ = cgls_fused(prob, g, max_iter=sched[0], restart_iter=sched[1], check_every=False)
-    monkeypatch.setenv("GSLM_CG_SIDE_X", "0")
-    x_inplace, _ = cgls_fused(prob, g, max_iter=sched[0], restart_iter=sched[1], check_every=False)
-    x_chk, _ = cgls_fused(prob, g, max_iter=sched[0], restart_iter=sched[1], check_every=True)
-    assert torch.equal(x_side, x_inplace)
-    assert torch.equal(x_side, x_chk)
-
-
 def test_cg_nocheck_matches_checked():
     """Benchmark mode (no host sync per iteration) produces the same iterates."""
     from gslm.lm import LMProblem, cgls_fused
