@@ -21,6 +21,7 @@ separately (gaussian_renderer/__init__.py:82-100): the rasterizer reads both in 
 forward-mode JVP), so the LM path is unchanged by it.
 """
 import ctypes
+import os
 from typing import NamedTuple
 
 import torch
@@ -90,6 +91,16 @@ def forward_buffers(view, g, device):
     return color, radii, invdepth, geom, binning, image, N
 
 
+_BWD_MEMO = os.environ.get("GSLM_BWD_MEMO", "1") != "0"
+
+
+def _same_cotangent(a, b):
+    """Equal cotangents (both absent, or the same shape and every element equal; one device compare and read-back)."""
+    if a is None or b is None:
+        return a is None and b is None
+    return a.shape == b.shape and a.dtype == b.dtype and a.device == b.device and bool(torch.equal(a, b))
+
+
 def _cpu_copy(args):
     return tuple(a.detach().cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
 
@@ -153,6 +164,24 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_color, _grad_radii, grad_invdepth, *_unused):
+        # The reference's J^T v (solver_functions.py:101-132) calls backward twice on one graph, once per half of the
+        # [r; r] pair (loss_image_state.py:93-97), and with disable_ssim the halves are the same image
+        # (batch_training_loss.py:15-17), so every such pair of calls brings equal cotangents.  The VJP is a
+        # deterministic function of the saved forward and the cotangent: a call whose cotangents equal the previous
+        # call's, element for element (compared on the device), returns that call's gradients -- bitwise what the
+        # kernels would produce again.  They stay referenced here until the graph is freed, so autograd clones them
+        # before accumulating and never writes into them.  GSLM_BWD_MEMO=0 turns it off.
+        memo = getattr(ctx, "bw_memo", None)
+        if memo is not None and _same_cotangent(memo[0], grad_color) and _same_cotangent(memo[1], grad_invdepth):
+            return memo[2]
+        out = _RasterizeGaussians._backward(ctx, grad_color, grad_invdepth)
+        if _BWD_MEMO:
+            ctx.bw_memo = (None if grad_color is None else grad_color.detach().clone(),
+                           None if grad_invdepth is None else grad_invdepth.detach().clone(), out)
+        return out
+
+    @staticmethod
+    def _backward(ctx, grad_color, grad_invdepth):
         (means3D, sh, dc, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, geom, binning,
          image) = ctx.saved_tensors
         st = ctx.raster_settings
