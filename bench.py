@@ -411,39 +411,7 @@ def main():
     del prob, loc, vr, vs, ys, x, xv, g
     torch.cuda.empty_cache()
 
-    # the raster forwards with RASTER_STREAMS renders in flight on as many HIP streams (the line search's setting:
-    # independent validation renders overlap, a render's launch-bound sort passes beside another's blend) -- a
-    # throughput over many renders, reported beside the one-stream rate, which stays `raster_mpix_s`.  Run after the
-    # roofline's kernel timing (which it would otherwise precede: the stage timing right after this burst of 8-stream
-    # work measured k_render_matvec 7% slower than rocprof's solo average) and with the problem's memory released
     raster_streams = None
-    if not args.no_side and view0 is not None:
-        from gslm.lm import ViewRaster
-        S = RASTER_STREAMS
-        rasters = [ViewRaster(view0, device) for _ in range(S)]
-        streams = [torch.cuda.Stream(device) for _ in range(S)]
-        for r, st in zip(rasters, streams):
-            r.forward(graw, st.cuda_stream)
-        capz = [r.capacity() for r in rasters]
-        cnt_s = torch.zeros(max(fsteps, 1) * S, dtype=torch.int32, device=device)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for it in range(fsteps):
-            for j, (r, st) in enumerate(zip(rasters, streams)):
-                r.forward_dev(graw, st.cuda_stream, n_out=cnt_s.data_ptr() + 4 * (it * S + j))
-        torch.cuda.synchronize()
-        t_s = time.perf_counter() - t0
-        cs = cnt_s.view(max(fsteps, 1), S).tolist()
-        if any(c[j] > capz[j] for c in cs[:fsteps] for j in range(S)):
-            raise RuntimeError("raster_streams: a pair count exceeded its list capacity")
-        raster_streams = {"streams": S, "renders": S * fsteps, "mpix_s": S * fsteps * W * H / t_s / 1e6,
-                          "ms_per_render": 1e3 * t_s / (S * fsteps),
-                          "note": f"{S} independent forwards of view 0 in flight on {S} HIP streams (gslm_rasterize_dev, "
-                                  "counts checked after the loop): render throughput, not one forward's latency "
-                                  "(raster_mpix_s / forward_ms_per_view)"}
-        del rasters, streams
-        torch.cuda.empty_cache()
-
 
     fb = c0_gpu = lm = lm_tv = lm_ref = ssim = fo = dropin = None
     if not args.no_side:
@@ -488,6 +456,41 @@ def main():
     rank_slices = None
     if world_size == 1 and not forced and not args.no_side and not args.no_rank_slices:
         rank_slices = rank_slice_memory(model, cams_all, val_all, bg, device)
+
+    # ---------------- the raster forwards with RASTER_STREAMS renders in flight on as many HIP streams (independent
+    # renders overlap, a render's launch-bound sort passes beside another's blend) -- a throughput over many renders,
+    # reported beside the one-stream rate, which stays `raster_mpix_s`.  Run LAST among the GPU measurements: after a
+    # burst of 8-stream work the process's later kernels run slower (the stage timing measured k_render_matvec 7% over
+    # rocprof's solo average; the LM step 96.3 ms against 91-92 in tools/exp/lm_phases.py on the same box, every
+    # phase 6-10% slower, profiles/r06/ab_bench_order/), which an LM run that never issues such a burst does not see
+    if not args.no_side and view0 is not None:
+        from gslm.lm import ViewRaster
+        S = RASTER_STREAMS
+        rasters = [ViewRaster(view0, device) for _ in range(S)]
+        graw2 = raw_gaussians(model)
+        streams = [torch.cuda.Stream(device) for _ in range(S)]
+        for r, st in zip(rasters, streams):
+            r.forward(graw2, st.cuda_stream)
+        capz = [r.capacity() for r in rasters]
+        cnt_s = torch.zeros(max(fsteps, 1) * S, dtype=torch.int32, device=device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(fsteps):
+            for j, (r, st) in enumerate(zip(rasters, streams)):
+                r.forward_dev(graw2, st.cuda_stream, n_out=cnt_s.data_ptr() + 4 * (it * S + j))
+        torch.cuda.synchronize()
+        t_s = time.perf_counter() - t0
+        cs = cnt_s.view(max(fsteps, 1), S).tolist()
+        if any(c[j] > capz[j] for c in cs[:fsteps] for j in range(S)):
+            raise RuntimeError("raster_streams: a pair count exceeded its list capacity")
+        raster_streams = {"streams": S, "renders": S * fsteps, "mpix_s": S * fsteps * W * H / t_s / 1e6,
+                          "ms_per_render": 1e3 * t_s / (S * fsteps),
+                          "note": f"{S} independent forwards of view 0 in flight on {S} HIP streams (gslm_rasterize_dev, "
+                                  "counts checked after the loop): render throughput, not one forward's latency "
+                                  "(raster_mpix_s / forward_ms_per_view)"}
+        del rasters, streams
+        torch.cuda.empty_cache()
+
 
     # ---------------- CPU baseline (rank 0, N = 1 only): the oracle on host cores, bounded sample
     cpu = None
