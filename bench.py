@@ -442,7 +442,7 @@ def main():
         # evaluate_loss (tests/test_jvp_timing.py:71-106 through the reference's call shapes)
         torch.cuda.reset_peak_memory_stats(device)
         resident = torch.cuda.memory_allocated(device)
-        dropin = time_dropin_solver_ops(model, cams[0], bg) if rank == 0 else None
+        dropin = time_dropin_solver_ops(model, cams[0], bg, reps=11) if rank == 0 else None
         peak_mem["dropin_solver_ops"] = {"max_allocated_gb": peak_gb(device), "resident_before_gb": resident / 1e9,
                                          "note": "the drop-in J u / J^T v / forward calls through render() at the "
                                                  "headline size (autograd graphs, dual tensors, rasterizer buffers)"}
