@@ -42,7 +42,7 @@ def main():
     print(sep)
     for (t, q), (m, b) in sorted(base.items(), key=lambda kv: (kv[1][1] / kv[1][0]) if kv[1][0] > 0 else 1e30):
         head = f"{b / m:.0f}x" if m > 0 else "exact"
-        row = f"| `{t}` | {q} | {b:.0e} | {m:.2e} | {head} |"
+        row = f"| `{t}` | {q} | {b:.3g} | {m:.2e} | {head} |"
         if pert:
             pm = pert.get((t, q))
             row += (f" {pm[0]:.2e} |" if pm else " -- |")
