@@ -55,7 +55,10 @@ __device__ __forceinline__ void load_group(const float* v, const float* y, int64
   }
 }
 
-// y = (overwrite ? 0 : y_old) + val + d v; returns sum of v * y_new (0 when dot is off)
+// y = (overwrite ? 0 : y_old) + val + d v; returns sum of v * y_new (0 when dot is off).  y is stored nontemporal:
+// the gather's output is not re-read before the next kernel boundary writes the L2s back; measured -7 us on the
+// gather and -2.7 us per CG iteration (4 of 4 alternations; nontemporal gradient rows, which the gather reads at
+// once, cost +20 us: profiles/r06/ab_nontemporal_stores/)
 template <int K>
 __device__ __forceinline__ double store_group(float* y, float d, int use_damp, int64_t base, int overwrite, bool dot,
                                               const float val[K], const float vin[K], const float yold[K]) {
@@ -65,7 +68,7 @@ __device__ __forceinline__ double store_group(float* y, float d, int use_damp, i
     float x = val[k];
     if (use_damp) x += d * vin[k];
     const float out = overwrite ? x : yold[k] + x;
-    y[base + k] = out;
+    __builtin_nontemporal_store(out, &y[base + k]);  // streamed (profiles/r06/ab_nontemporal_stores/)
     if (dot) acc += (double)vin[k] * (double)out;
   }
   return acc;
@@ -219,7 +222,7 @@ __device__ __forceinline__ void lm_epilogue(int nc, const GaussK& g, const Chain
         }
         if (u) val += o.damp[2] * vin[k];
         const float out = ow ? val : yold[k] + val;
-        o.y[2][base + e] = out;
+        __builtin_nontemporal_store(out, &o.y[2][base + e]);
         if (dot) dacc += (double)vin[k] * (double)out;
       }
     }
