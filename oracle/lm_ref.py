@@ -79,7 +79,14 @@ class OracleLMProblem:
         leaves = self._leaves()
         for t in leaves:
             t.grad = None
-        loss = sum((0.5 * self._fac) * (r * r).sum() for r in self._residuals())  # J^T b = -grad
+        res = list(self._residuals())
+        if not res:  # a rank holding no views (an uneven split): J^T b = 0
+            g = torch.zeros(self.layout.numel)
+            if out is not None:
+                out.copy_(g)
+                return out
+            return g
+        loss = sum((0.5 * self._fac) * (r * r).sum() for r in res)  # J^T b = -grad
         grads = torch.autograd.grad(loss, leaves, allow_unused=True)
         g = self._flatten([-(gr if gr is not None else torch.zeros_like(t)) for gr, t in zip(grads, leaves)])
         g = self._mask(g.detach())
@@ -111,6 +118,11 @@ class OracleLMProblem:
     def local_normal_matvec(self, v, y, damp=False):
         """y = [D v +] sum_b 2 J_r^T J_r v (overwrites y)."""
         v = self._mask(v.clone())
+        if not self.cams:  # no views: J^T J v = 0
+            y.zero_()
+            if damp:
+                self.damp_add(v, y)
+            return y
         jv = self._jr_v(v)
         leaves = self._leaves()
         res = self._residuals()

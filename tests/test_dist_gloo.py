@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the view-sharded LM operator (gslm.parallel.ShardedOperator) equals the
+"""CPU, world_size 2-4 (gloo): the view-sharded LM operator (gslm.parallel.ShardedOperator) equals the
 single-process operator over the whole view batch -- loss, J^T b, (J^T J + D) v and a CG solve.
 The per-rank operator is the oracle restatement (oracle.lm_ref), the sharding/reduction code is the
 product's."""
@@ -76,13 +76,16 @@ def _worker(rank, world, port, out_path, ssim=False, exchange="allreduce"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ssim,exchange", [(False, "allreduce"), (True, "allreduce"), (False, "gaussian")])
-def test_sharded_operator_matches_single_process(tmp_path, ssim, exchange):
+@pytest.mark.parametrize("ssim,exchange,world", [(False, "allreduce", 2), (True, "allreduce", 2), (False, "gaussian", 2),
+                                               (False, "allreduce", 3), (False, "gaussian", 4)])
+def test_sharded_operator_matches_single_process(tmp_path, ssim, exchange, world):
     """Both residuals: disable_ssim=True ([r; r]) and the SSIM residual ([r1; r2]); and the
-    Gaussian-sharded vector layout (gslm.parallel.GaussianShardedOperator)."""
+    Gaussian-sharded vector layout (gslm.parallel.GaussianShardedOperator).  World sizes 3 (the 4 views
+    split 2 + 1 + 1: the replicated-vector exchange, as the driver's uneven splits take it) and 4 (one view per rank,
+    300 Gaussians in shards of 75: the Gaussian-sharded exchange as the n = 4 bench runs it)."""
     from oracle.lm_ref import OracleLMProblem, cgls_ref
     out = str(tmp_path / "r0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), out, ssim, exchange), nprocs=2, start_method="spawn",
+    mp.start_processes(_worker, args=(world, _free_port(), out, ssim, exchange), nprocs=world, start_method="spawn",
                        join=True)
     got = torch.load(out, weights_only=True)
     model, cams = _scene()
@@ -144,25 +147,28 @@ def _lm_step_worker(rank, world, port, out_path, tag, sched):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("tag,sched", [("ref", (2, 1)), ("ten", (10, 10))])
-def test_sharded_lm_step_matches_reference_golden(tmp_path, tag, sched):
+@pytest.mark.parametrize("tag,sched,world", [("ref", (2, 1), 2), ("ten", (10, 10), 2), ("ten", (10, 10), 3)])
+def test_sharded_lm_step_matches_reference_golden(tmp_path, tag, sched, world):
     """gslm.lm.lm_step across 2 ranks (train_jvp.py:237-279, SURVEY 8(e) 'Line search. Sharded the same way'): one
     training view per rank with Gaussian-sharded CG vectors, the 3 validation views split 2 + 1 with one all-reduced
     loss per line-search point, the step gathered whole and applied on both ranks.  Both ranks must end with
     bitwise identical parameters, and the step, best_alpha, search trace, final loss and parameters must match
     the reference's (lm_step_golden.npz) at the single-process GPU test's tolerances.  The per-rank problem is the
-    oracle restatement; the driver, sharding and reductions are the product's."""
+    oracle restatement; the driver, sharding and reductions are the product's.  At world size 3 the 2 training views
+    leave one rank without a training view (the replicated-vector exchange) and the 3 validation views go 1 + 1 + 1."""
     import numpy as np
     out = str(tmp_path / "r")
-    mp.start_processes(_lm_step_worker, args=(2, _free_port(), out, tag, sched), nprocs=2, start_method="spawn",
+    mp.start_processes(_lm_step_worker, args=(world, _free_port(), out, tag, sched), nprocs=world, start_method="spawn",
                        join=True)
-    r0, r1 = (torch.load(out + f".{r}", weights_only=True) for r in (0, 1))
-    for a, b in zip(r0["params"], r1["params"]):
-        assert torch.equal(a, b)
-    assert torch.equal(r0["step"], r1["step"])
+    rs = [torch.load(out + f".{r}", weights_only=True) for r in range(world)]
+    r0 = rs[0]
+    for r1 in rs[1:]:
+        for a, b in zip(r0["params"], r1["params"]):
+            assert torch.equal(a, b)
+        assert torch.equal(r0["step"], r1["step"])
     L = np.load(os.path.join(HERE, "golden", "lm_step_golden.npz"))
     o = r0["out"]
-    assert o["ranks"] == 2
+    assert o["ranks"] == world
     assert abs(o["start_loss"] - float(L[f"{tag}_start_loss"])) <= 1e-5 * float(L[f"{tag}_start_loss"])
     s_ref = L[f"{tag}_s"].astype(np.float64)
     s = r0["step"].numpy().astype(np.float64)
