@@ -306,23 +306,49 @@ int gslm_num_rendered(const void* geom, int64_t P, int64_t* out, void* stream) {
   return GSLM_OK;
 }
 
+}  // extern "C"
+
+namespace gslm {
+constexpr int READ_COUNTS_MAX = 32;
+struct CountPtrs {
+  const uint32_t* p[READ_COUNTS_MAX];
+};
+// the pair counts of up to 32 geometries into pinned host memory in ONE launch (thread k: count k), where one
+// 4-byte device-to-host copy per geometry is a blit launch each, in series on the stream
+__global__ void k_read_counts(CountPtrs c, int n, uint32_t* __restrict__ out) {
+  const int k = threadIdx.x;
+  if (k < n) out[k] = *c.p[k];
+}
+}  // namespace gslm
+
+extern "C" {
+
 int gslm_num_rendered_many(const void* const* geoms, const int64_t* Ps, int32_t n, int64_t* out, void* stream) {
   if (n < 0 || (n > 0 && (!geoms || !Ps || !out))) { set_error("num_rendered_many: NULL argument"); return GSLM_ERR_INVALID; }
   if (n == 0) return GSLM_OK;
-  // one pinned array per host thread, grown on demand: n small copies, then ONE stream sync
+  // one pinned array per host thread, grown on demand: one gather launch per 32 geometries writing into it, then
+  // ONE stream sync
   thread_local uint32_t* pinned = nullptr;
+  thread_local uint32_t* pinned_dev = nullptr;
   thread_local int32_t cap = 0;
   if (cap < n) {
     if (pinned) GSLM_HIP_CHECK(hipHostFree(pinned));
-    pinned = nullptr;
+    pinned = pinned_dev = nullptr;
     cap = 0;
     GSLM_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t) * (size_t)n, hipHostMallocDefault));
+    GSLM_HIP_CHECK(hipHostGetDevicePointer((void**)&pinned_dev, pinned, 0));
     cap = n;
   }
-  for (int32_t k = 0; k < n; ++k) {
-    GeomBufs gb;
-    geom_layout(Ps[k], const_cast<void*>(geoms[k]), &gb);
-    GSLM_HIP_CHECK(hipMemcpyAsync(pinned + k, gb.counters, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  for (int32_t k0 = 0; k0 < n; k0 += READ_COUNTS_MAX) {
+    CountPtrs c{};
+    const int m = n - k0 < READ_COUNTS_MAX ? n - k0 : READ_COUNTS_MAX;
+    for (int k = 0; k < m; ++k) {
+      GeomBufs gb;
+      geom_layout(Ps[k0 + k], const_cast<void*>(geoms[k0 + k]), &gb);
+      c.p[k] = gb.counters;
+    }
+    hipLaunchKernelGGL(k_read_counts, dim3(1), dim3(64), 0, (hipStream_t)stream, c, m, pinned_dev + k0);
+    GSLM_LAUNCH_CHECK();
   }
   GSLM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   for (int32_t k = 0; k < n; ++k) out[k] = (int64_t)pinned[k];
