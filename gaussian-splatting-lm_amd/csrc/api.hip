@@ -162,11 +162,15 @@ int do_preprocess(const ViewK& v, const GaussK& g, const GeomBufs& gb, int32_t* 
     GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, depth_order, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
   } else {
     // depth sort of (key, index) pairs: the first scatter generates the indices (no iota pass), the last writes
-    // tiles[index] where the sorted keys would go.  (Round 6 measured 3 passes of 11-bit digits against these 4 of 8
-    // bits: 90.9 against 90.8 us per 1M keys -- the 2048-digit scatter and scan cost what the fourth pass did --
+    // tiles[index] where the sorted keys would go.  key_range: the passes sort the bytes of key - min and those past
+    // the frame's span run as copies (the 32-bit order exactly; sort.hip KeyRange): 3 working passes at the bench
+    // scene's depths, -7 us per forward (profiles/r06/ab_depth_key_range/; routing the working passes through a third
+    // buffer pair instead of copying measured the same).  (Round 6 also measured 3 passes of 11-bit digits against 4 of
+    // 8 bits: 90.9 against 90.8 us per 1M keys -- the 2048-digit scatter and scan cost what the fourth pass did --
     // profiles/r06/ab_depth_sort_d11_neutral/.)
     bool alt = false;
-    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true, gb.tiles);
+    st = radix_sort_pairs(gb.depth_key, gb.vals_init, gb.keys_alt, gb.vals_alt, P, 32, gb.hist, &alt, s, true, gb.tiles,
+                          nullptr, nullptr, nullptr, true);
     if (st) return st;
     if (alt) GSLM_HIP_CHECK(hipMemcpyAsync(gb.sorted_idx, gb.vals_alt, (size_t)P * 4, hipMemcpyDeviceToDevice, s));
     tiles_sorted = alt ? gb.keys_alt : gb.depth_key;

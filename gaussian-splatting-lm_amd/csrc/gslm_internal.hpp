@@ -70,8 +70,11 @@ inline int64_t sort_blocks(int64_t n, bool payload = false) {
   const int64_t t = (int64_t)SORT_THREADS * sort_items(n, payload);
   return (n + t - 1) / t;
 }
+// [RADIX][blocks] counts, RADIX digit totals, then the key range of a key_range sort: 4 words and a (min, max) pair
+// per block
 inline size_t sort_hist_bytes(int64_t n, bool payload = false) {
-  return (size_t)RADIX * (size_t)sort_blocks(n, payload) * 4 + 4 * RADIX;
+  const size_t nb = (size_t)sort_blocks(n, payload);
+  return (size_t)RADIX * nb * 4 + 4 * RADIX + 16 + 8 * nb;
 }
 
 // Sorts (keys, vals) of length n on bits [0, end_bit).  Uses k0/v0 as input and k1/v1 as the
@@ -80,10 +83,13 @@ inline size_t sort_hist_bytes(int64_t n, bool payload = false) {
 // n_dev (or NULL): n is a capacity (grid and hist sized for it) and the kernels sort the first min(n, *n_dev) pairs.
 // p0 / p1 (or NULL): a second value array (p0 input, p1 its ping-pong partner) moved with the pairs; the result is
 // in p1 exactly when *result_in_alt.
+// key_range (the depth sort: end_bit 32, no n_dev / payload): the passes sort key - min over the keys other than
+// 0xFFFFFFFF (those sort last, as before), and the passes past the span's bytes run as copies -- the 32-bit sort's
+// order bit for bit, in fewer working passes when the keys span fewer than 32 bits (sort.hip KeyRange).
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
                      uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values = false,
                      const uint32_t* last_gather = nullptr, const uint32_t* n_dev = nullptr, uint32_t* p0 = nullptr,
-                     uint32_t* p1 = nullptr);
+                     uint32_t* p1 = nullptr, bool key_range = false);
 
 // ---------------- exclusive scan of uint32 (optionally gathered through idx) ----------------
 constexpr int SCAN_THREADS = 256;

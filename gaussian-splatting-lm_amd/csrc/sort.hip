@@ -90,32 +90,123 @@ __global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ bs, int
   }
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor(x, o, 64));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor(x, o, 64));
+  return x;
+}
+
+// The depth sort's key range (radix_sort_pairs(..., key_range = true); VERDICT r05 item 2: sort only the bits the
+// frame's depths use).  Pass 0 sorts the low byte of key - kmin, which is the raw low byte rotated by kmin's: its
+// histogram kernel counts raw digits and records each block's (min, max) over the keys other than 0xFFFFFFFF (the
+// Gaussians behind the near plane), and block 0 of its scan reduces those into w: kmin, the sort value t of the
+// 0xFFFFFFFF keys (the least value past max - kmin whose low byte is (0xFF - kmin) mod 256, so pass 0's rotation
+// holds for them too) and the working pass count (the bytes of t).  Later passes sort the bytes of
+// key' = key - kmin (t for 0xFFFFFFFF), monotone in key with the 0xFFFFFFFF keys last: the stable order is the
+// 32-bit sort's.  Past the working passes every key' byte is 0 and the pass is the identity: the histogram and scan
+// kernels return at once and the scatter copies (same ping-pong parity, the last pass's gather kept).
+struct KeyRange {
+  uint32_t* w;   // [0] kmin, [1] t, [2] working passes
+  uint2* blk;    // [blocks] (min, max) of each pass-0 histogram block's keys other than 0xFFFFFFFF
+  int pass;
+};
+__device__ __forceinline__ uint32_t range_key(uint32_t k, uint32_t kmin, uint32_t t) {
+  return k == 0xFFFFFFFFu ? t : k - kmin;
+}
+
 // n_dev (or NULL): the key count is min(n, *n_dev), read on the device (a capacity-sized launch whose count the host
 // has not read back: gslm_rasterize_dev); blocks past it count nothing
-template <int ITEMS>
+template <int ITEMS, bool RANGE = false>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, int64_t n,
                                                              int shift, uint32_t dmask, uint32_t* __restrict__ hist,
-                                                             int nblocks, const uint32_t* __restrict__ n_dev) {
+                                                             int nblocks, const uint32_t* __restrict__ n_dev,
+                                                             KeyRange kr = KeyRange{}) {
   __shared__ uint32_t cnt[RADIX];
+  __shared__ uint32_t s_mm[2][4];
   const int tid = threadIdx.x;
+  uint32_t kmin = 0u, t = 0u;
+  if (RANGE && kr.pass > 0) {
+    if (kr.pass >= (int)kr.w[2]) return;  // past the span (block-uniform)
+    kmin = kr.w[0];
+    t = kr.w[1];
+  }
   if (n_dev) n = min(n, (int64_t)*n_dev);
   cnt[tid] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * (SORT_THREADS * ITEMS);
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #pragma unroll 4
   for (int r = 0; r < ITEMS; ++r) {
     const int64_t i = base + r * SORT_THREADS + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & dmask], 1u);
+    if (i < n) {
+      const uint32_t k = keys[i];
+      if (RANGE && kr.pass == 0 && k != 0xFFFFFFFFu) {
+        lo = min(lo, k);
+        hi = max(hi, k);
+      }
+      const uint32_t kk = (RANGE && kr.pass > 0) ? range_key(k, kmin, t) : k;  // pass 0: the raw digit
+      atomicAdd(&cnt[(kk >> shift) & dmask], 1u);
+    }
+  }
+  if (RANGE && kr.pass == 0) {
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    if ((tid & 63) == 0) {
+      s_mm[0][tid >> 6] = lo;
+      s_mm[1][tid >> 6] = hi;
+    }
   }
   __syncthreads();
   hist[(int64_t)tid * nblocks + blockIdx.x] = cnt[tid];
+  if (RANGE && kr.pass == 0 && tid == 0)
+    kr.blk[blockIdx.x] = make_uint2(min(min(s_mm[0][0], s_mm[0][1]), min(s_mm[0][2], s_mm[0][3])),
+                                    max(max(s_mm[1][0], s_mm[1][1]), max(s_mm[1][2], s_mm[1][3])));
 }
 
 // One block per digit: exclusive scan of that digit's per-block counts; digit total -> totals[d].
+// RANGE, pass 0: block 0 first reduces the histogram blocks' key ranges into kr.w (KeyRange).
+template <bool RANGE = false>
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int nblocks,
-                                                    uint32_t* __restrict__ totals) {
+                                                    uint32_t* __restrict__ totals, KeyRange kr = KeyRange{}) {
   __shared__ uint32_t s_w[4];
   const int d = blockIdx.x, tid = threadIdx.x;
+  if (RANGE && kr.pass > 0 && kr.pass >= (int)kr.w[2]) return;
+  if (RANGE && kr.pass == 0 && d == 0) {
+    __shared__ uint32_t s_mm[2][4];
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    for (int b = tid; b < nblocks; b += 256) {
+      const uint2 m = kr.blk[b];
+      lo = min(lo, m.x);
+      hi = max(hi, m.y);
+    }
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    if ((tid & 63) == 0) {
+      s_mm[0][tid >> 6] = lo;
+      s_mm[1][tid >> 6] = hi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      lo = min(min(s_mm[0][0], s_mm[0][1]), min(s_mm[0][2], s_mm[0][3]));
+      hi = max(max(s_mm[1][0], s_mm[1][1]), max(s_mm[1][2], s_mm[1][3]));
+      uint32_t kmin = 0u, t = 0xFFu;  // no key other than 0xFFFFFFFF: one digit value, one pass
+      if (lo <= hi) {
+        kmin = lo;
+        const uint32_t r1 = hi - kmin + 1u;              // past every other key's key'
+        const uint32_t lowb = (0xFFu - kmin) & 0xFFu;    // (0xFFFFFFFF - kmin) mod 256
+        t = r1 + ((lowb - r1) & 0xFFu);                  // <= 0xFFFFFFFF - kmin: no wrap
+      }
+      const int bits = 32 - __clz((int)t);
+      kr.w[0] = kmin;
+      kr.w[1] = t;
+      kr.w[2] = (uint32_t)max(1, (bits + 7) / 8);
+    }
+  }
   uint32_t* h = hist + (int64_t)d * nblocks;
   uint32_t carry = 0;
   // up to 8 chunks of 256 counts loaded together (the tile sort's ~1200 blocks: 5 chunks, one load latency instead of
@@ -150,12 +241,14 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // threads (coalesced segments instead of one scattered 4-byte store per key).
 // PAY: a second value array moves with the pairs (pin -> pout; the line search's union list carries each entry's
 // per-set quadrant masks through the tile sort, gslm_union_binning).
-template <int ITEMS, bool PAY = false>
+// RANGE: the digits of key' (KeyRange; pass 0 the low byte of key - kmin, i.e. digit run d' holds raw digit
+// (d' + kmin) mod 256's counts); past the working passes a plain copy.
+template <int ITEMS, bool PAY = false, bool RANGE = false>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, int nbits, const uint32_t* __restrict__ hist, int nblocks,
     const uint32_t* __restrict__ totals, const uint32_t* __restrict__ kgather, const uint32_t* __restrict__ n_dev,
-    const uint32_t* __restrict__ pin = nullptr, uint32_t* __restrict__ pout = nullptr) {
+    const uint32_t* __restrict__ pin = nullptr, uint32_t* __restrict__ pout = nullptr, KeyRange kr = KeyRange{}) {
   static_assert(SORT_THREADS == 256 && RADIX == 256, "one digit per thread, four waves");
   constexpr int TILE = SORT_THREADS * ITEMS;
   constexpr int WAVE_KEYS = TILE / 4;
@@ -171,6 +264,29 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   const int nvalid = (int)max<int64_t>(-1, min<int64_t>(TILE, n - base));
   const int wbase = w * WAVE_KEYS;
   const uint32_t dmask = (1u << nbits) - 1u;
+  uint32_t kmin = 0u, kt = 0u, rot = 0u;
+  if (RANGE) {
+    kmin = kr.w[0];
+    kt = kr.w[1];
+    if (kr.pass >= (int)kr.w[2]) {  // past the span: the identity pass (block-uniform)
+      for (int e = tid; e < TILE; e += SORT_THREADS) {
+        const int64_t i = base + e;
+        if (i < n) {
+          const uint32_t val = vin ? vin[i] : (uint32_t)i;
+          kout[i] = kgather ? kgather[val] : kin[i];
+          vout[i] = val;
+        }
+      }
+      return;
+    }
+    if (kr.pass == 0) rot = kmin & 0xFFu;
+  }
+  // this pass's digit of a key
+  auto digit = [&](uint32_t k) -> uint32_t {
+    if (!RANGE) return (k >> shift) & dmask;
+    if (kr.pass == 0) return (k - kmin) & dmask;  // == key' & dmask, the 0xFFFFFFFF keys included (t's low byte)
+    return (range_key(k, kmin, kt) >> shift) & dmask;
+  };
 
 #pragma unroll
   for (int k = 0; k < 4; ++k) s_wcnt[w][lane + 64 * k] = 0u;
@@ -187,17 +303,18 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
   {
     // global base of each digit's run for this block = exclusive prefix of digit totals + this block's offset
-    const uint32_t t = totals[tid];
+    const uint32_t draw = (tid + rot) & 0xFFu;  // the raw digit whose counts digit run tid holds (rot 0: itself)
+    const uint32_t t = totals[draw];
     uint32_t tot;
     const uint32_t inc = block_incl_scan256(t, s_w, &tot);
-    s_gbase[tid] = inc - t + hist[(int64_t)tid * nblocks + blockIdx.x];
+    s_gbase[tid] = inc - t + hist[(int64_t)draw * nblocks + blockIdx.x];
   }
   // 1. wave-local stable rank of every key among equal digits
   const unsigned long long lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const bool valid = wbase + r * 64 + lane < nvalid;
-    const uint32_t d = (key[r] >> shift) & dmask;
+    const uint32_t d = digit(key[r]);
     unsigned long long m = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -229,7 +346,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     if (wbase + r * 64 + lane < nvalid) {
-      const uint32_t d = (key[r] >> shift) & dmask;
+      const uint32_t d = digit(key[r]);
       const uint32_t lp = s_loc[d] + s_wcnt[w][d] + lrank[r];
       s_keys[lp] = key[r];
       s_vals[lp] = val[r];
@@ -240,7 +357,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   // 3. each run to its global offset, consecutive threads on consecutive elements
   for (int e = tid; e < nvalid; e += SORT_THREADS) {
     const uint32_t k = s_keys[e];
-    const uint32_t d = (k >> shift) & dmask;
+    const uint32_t d = digit(k);
     const uint32_t pos = s_gbase[d] + ((uint32_t)e - s_loc[d]);
     const uint32_t val = s_vals[e];
     // kgather (the last pass of the depth sort): the sorted keys are not needed afterwards, so their slot carries
@@ -423,15 +540,37 @@ int exclusive_scan_u32_dual(const uint32_t* in, const uint32_t* idx, uint32_t* o
   return GSLM_OK;
 }
 
+// one pass of a key_range sort (KeyRange)
+template <int ITEMS>
+static void launch_range_pass(const uint32_t* ki, const uint32_t* vin, uint32_t* ko, uint32_t* vo, int64_t n, int shift,
+                              int nbits, uint32_t dmask, uint32_t* hist, int nb, uint32_t* totals, const uint32_t* kg,
+                              KeyRange kr, hipStream_t s) {
+  hipLaunchKernelGGL((k_radix_hist<ITEMS, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb,
+                     (const uint32_t*)nullptr, kr);
+  hipLaunchKernelGGL(k_radix_scan<true>, dim3(RADIX), dim3(256), 0, s, hist, nb, totals, kr);
+  hipLaunchKernelGGL((k_radix_scatter<ITEMS, false, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n, shift,
+                     nbits, hist, nb, totals, kg, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                     kr);
+}
+
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int end_bit,
                      uint32_t* hist, bool* result_in_alt, hipStream_t s, bool iota_values, const uint32_t* last_gather,
-                     const uint32_t* n_dev, uint32_t* p0, uint32_t* p1) {
+                     const uint32_t* n_dev, uint32_t* p0, uint32_t* p1, bool key_range) {
   *result_in_alt = false;
   if (n <= 0) return GSLM_OK;
   const bool pay = p0 != nullptr;
+  if (key_range && (pay || n_dev || end_bit != 32)) {
+    set_error("radix_sort_pairs: key_range needs 32-bit keys, no payload, a host-known count");
+    return GSLM_ERR_INVALID;
+  }
   const int nb = (int)sort_blocks(n, pay);
   const bool small = sort_items(n, pay) != SORT_ITEMS;
   uint32_t* totals = hist + (size_t)RADIX * nb;
+  KeyRange kr{};
+  if (key_range) {
+    kr.w = totals + RADIX;
+    kr.blk = reinterpret_cast<uint2*>(kr.w + 4);
+  }
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1, *pi = p0, *po = p1;
   bool first = true;  // iota_values: the first scatter generates value = index instead of reading v0
   bool alt = false;
@@ -444,10 +583,14 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
     const uint32_t dmask = (1u << nbits) - 1u;
     const uint32_t* vin = (first && iota_values) ? (const uint32_t*)nullptr : vi;
     const uint32_t* kg = (shift + per >= end_bit) ? last_gather : nullptr;  // the last pass
-    if (small) {
+    if (key_range) {
+      if (small) launch_range_pass<SORT_ITEMS_SMALL>(ki, vin, ko, vo, n, shift, nbits, dmask, hist, nb, totals, kg, kr, s);
+      else launch_range_pass<SORT_ITEMS>(ki, vin, ko, vo, n, shift, nbits, dmask, hist, nb, totals, kg, kr, s);
+      ++kr.pass;
+    } else if (small) {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS_SMALL>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb,
                          n_dev);
-      hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+      hipLaunchKernelGGL(k_radix_scan<false>, dim3(RADIX), dim3(256), 0, s, hist, nb, totals, KeyRange{});
       if (pay)
         hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS_SMALL, true>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo,
                            n, shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)pi, po);
@@ -456,7 +599,7 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int
                            vo, n, shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
     } else {
       hipLaunchKernelGGL(k_radix_hist<SORT_ITEMS>, dim3(nb), dim3(SORT_THREADS), 0, s, ki, n, shift, dmask, hist, nb, n_dev);
-      hipLaunchKernelGGL(k_radix_scan, dim3(RADIX), dim3(256), 0, s, hist, nb, totals);
+      hipLaunchKernelGGL(k_radix_scan<false>, dim3(RADIX), dim3(256), 0, s, hist, nb, totals, KeyRange{});
       hipLaunchKernelGGL((k_radix_scatter<SORT_ITEMS, false>), dim3(nb), dim3(SORT_THREADS), 0, s, ki, vin, ko, vo, n,
                          shift, nbits, hist, nb, totals, kg, n_dev, (const uint32_t*)nullptr, (uint32_t*)nullptr);
     }
